@@ -1,0 +1,33 @@
+# Builds libfi_learner.so (HIP, gfx950 only) in-tree, plus the CPU oracle (test infra).
+# No cmake needed; `python -c "import __graft_entry__ as g; g.build()"` drives the same rules.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+CSRC := freeimpala_amd/csrc
+LIBDIR := freeimpala_amd/lib
+OBJDIR := build/obj
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude -I$(CSRC) -Wall -Wno-unused-result -Wno-unused-value \
+            -munsafe-fp-atomics
+SRCS := $(CSRC)/vtrace.hip $(CSRC)/gemm_f32.hip $(CSRC)/misc.hip $(CSRC)/atari.hip $(CSRC)/learner.cpp
+OBJS := $(patsubst $(CSRC)/%,$(OBJDIR)/%.o,$(SRCS))
+HDRS := $(wildcard $(CSRC)/*.h) include/fi_learner.h
+
+all: $(LIBDIR)/libfi_learner.so oracle
+
+$(OBJDIR)/%.hip.o: $(CSRC)/%.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/%.cpp.o: $(CSRC)/%.cpp $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(LIBDIR)/libfi_learner.so: $(OBJS)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+
+oracle:
+	$(MAKE) -s -C oracle
+
+clean:
+	rm -rf build $(LIBDIR)
+.PHONY: all oracle clean

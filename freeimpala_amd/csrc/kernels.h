@@ -1,0 +1,58 @@
+// kernels.h -- internal launchers of libfi_learner.so (not part of the C ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fi_learner.h"
+
+namespace fi {
+
+// the heads' upstream gradient: virtual [rows][A+1] = dlogits (TB rows, then 0) | dvalue
+struct HeadsGrad {
+    const float* dlog;  // (TB, A)
+    const float* dval;  // (rows)
+    int rows;           // (T+1)*B
+    int TB;             // T*B
+    int A;
+};
+
+// vtrace.hip
+size_t vtrace_workspace_bytes(int T, int B, int A);
+int vtrace_launch(int variant, int T, int B, int A, const float* pi, const float* mu,
+                  const int32_t* act, const float* rew, const float* disc, const float* val,
+                  const fi_vtrace_hparams& hp, float* vs, float* adv, float* dlog, float* dval,
+                  double* losses, void* ws, size_t ws_bytes, hipStream_t stream,
+                  bool finalize = true, int* nblk_out = nullptr);
+int vtrace_finalize_launch(void* ws, int nblk, double* losses, hipStream_t stream);
+
+// gemm_f32.hip (MLP, exact fp32)
+int f32_linear_fwd(const float* X, int M, int K, const float* W, const float* bias, int N,
+                   bool relu, float* Y, hipStream_t s);
+int f32_heads_fwd(const float* X, int M, int K, const float* W, const float* bias, int A,
+                  float* logits, float* values, hipStream_t s);
+int f32_linear_dgrad(const float* dY, int M, int N, const float* W, int K, const float* act,
+                     float* dX, hipStream_t s);
+int f32_heads_dgrad(const HeadsGrad& g, const float* W, int K, const float* act, float* dX,
+                    hipStream_t s);
+int f32_linear_wgrad_partial(const float* X, int M, int I, const float* dY, int N, int splits,
+                             float* slab, hipStream_t s);
+int f32_heads_wgrad_partial(const float* X, int I, const HeadsGrad& g, int splits, float* slab,
+                            hipStream_t s);
+
+// misc.hip
+int colsum_partial(const float* Y, int M, int N, int splits, float* slab, hipStream_t s);
+int heads_colsum_partial(const HeadsGrad& g, int splits, float* slab, hipStream_t s);
+int reduce_slabs(const float* slab, int splits, size_t count, float* out, hipStream_t s);
+int grad_sqnorm(const float* g, size_t n, double* part, int nblk, double* out, hipStream_t s);
+int optimizer_step(int opt, float* p, const float* g, float* m, float* v, size_t n, float lr,
+                   float b1, float b2, float eps, double bc1, double bc2, const double* sqnorm,
+                   float max_norm, hipStream_t s);
+int to_bf16(const float* src, uint16_t* dst, size_t n, hipStream_t s);
+int synth_launch(uint64_t seed, int T, int B, int B_glob, int b_off, int A, int D, float gamma,
+                 float* obs, float* mu, int32_t* act, float* rew, float* disc, uint8_t* frames,
+                 hipStream_t s);
+int ingest_launch(const void* rec, int T, int B, int A, int D, size_t entry_bytes, float* obs,
+                  float* mu, int32_t* act, float* rew, float* disc, hipStream_t s);
+
+}  // namespace fi

@@ -1,0 +1,329 @@
+// misc.hip -- HBM-bound helper kernels of the learner step (gfx950):
+//   * synthetic trajectories (Philox4x32-10, bit-identical to the oracle's generator)
+//   * ingest: (B, S*1024) SharedBuffer entries -> time-major SoA tensors
+//   * column sums / split-K slab reduction (deterministic, fixed order)
+//   * global gradient norm, Adam / SGD with global-norm clipping, fp32 -> bf16
+#include "fi_common.h"
+#include "kernels.h"
+
+namespace fi {
+
+// ---------------------------------------------------------------- Philox4x32-10
+__device__ __forceinline__ uint4 philox4(uint64_t seed, uint64_t e, uint32_t stream) {
+    uint32_t c0 = (uint32_t)e, c1 = (uint32_t)(e >> 32), c2 = stream, c3 = 0u;
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return make_uint4(c0, c1, c2, c3);
+}
+
+__device__ __forceinline__ float approx_normal(uint4 u) {
+    const uint32_t s = (u.x >> 8) + (u.y >> 8) + (u.z >> 8) + (u.w >> 8);
+    const float x = (float)((int32_t)s - (int32_t)(1u << 25));
+    return x * 0x1.bb67aep-24f;
+}
+
+enum { ST_OBS = 0, ST_MU = 1, ST_ACT = 2, ST_REW = 3, ST_DONE = 4, ST_FRAME = 5 };
+
+__global__ void synth_normal_kernel(uint64_t seed, uint32_t stream, int rows, int B, int B_glob,
+                                    int b_off, int D, float* out) {
+    const size_t n = (size_t)rows * B * D;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const size_t lrow = i / D;
+        const int d = (int)(i - lrow * D);
+        const int t = (int)(lrow / B), b = (int)(lrow - (size_t)t * B);
+        const uint64_t row = (uint64_t)t * B_glob + (uint64_t)(b_off + b);
+        out[i] = approx_normal(philox4(seed, row * D + d, stream));
+    }
+}
+
+__global__ void synth_scalar_kernel(uint64_t seed, int T, int B, int B_glob, int b_off, int A,
+                                    float gamma, int32_t* act, float* rew, float* disc) {
+    const size_t n = (size_t)T * B;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const int t = (int)(i / B), b = (int)(i - (size_t)t * B);
+        const uint64_t row = (uint64_t)t * B_glob + (uint64_t)(b_off + b);
+        if (act) {
+            const uint4 u = philox4(seed, row, ST_ACT);
+            act[i] = (int32_t)(((uint64_t)(u.x >> 8) * (uint32_t)A) >> 24);
+        }
+        if (rew) {
+            const uint4 u = philox4(seed, row, ST_REW);
+            rew[i] = (float)((int32_t)(u.x % 3u) - 1);
+        }
+        if (disc) {
+            const uint4 u = philox4(seed, row, ST_DONE);
+            disc[i] = ((u.x >> 8) < 167772u) ? 0.0f : gamma;
+        }
+    }
+}
+
+__global__ void synth_frames_kernel(uint64_t seed, int rows, int B, int B_glob, int b_off,
+                                    uint4* frames) {
+    constexpr int Q = 84 * 84 * 4 / 16;  // 16-byte pieces per frame
+    const size_t n = (size_t)rows * B * Q;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const size_t lrow = i / Q;
+        const int qd = (int)(i - lrow * Q);
+        const int t = (int)(lrow / B), b = (int)(lrow - (size_t)t * B);
+        const uint64_t row = (uint64_t)t * B_glob + (uint64_t)(b_off + b);
+        frames[i] = philox4(seed, row * Q + qd, ST_FRAME);
+    }
+}
+
+static int grid_for(size_t n) {
+    size_t g = (n + 255) / 256;
+    return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
+}
+
+int synth_launch(uint64_t seed, int T, int B, int B_glob, int b_off, int A, int D, float gamma,
+                 float* obs, float* mu, int32_t* act, float* rew, float* disc, uint8_t* frames,
+                 hipStream_t s) {
+    FI_REQUIRE(T >= 1 && B >= 1 && B_glob >= b_off + B && A >= 1, "synth: bad shape");
+    if (obs) {
+        FI_REQUIRE(D >= 1, "synth: D");
+        hipLaunchKernelGGL(synth_normal_kernel, dim3(grid_for((size_t)(T + 1) * B * D)), dim3(256), 0,
+                           s, seed, (uint32_t)ST_OBS, T + 1, B, B_glob, b_off, D, obs);
+    }
+    if (mu)
+        hipLaunchKernelGGL(synth_normal_kernel, dim3(grid_for((size_t)T * B * A)), dim3(256), 0, s,
+                           seed, (uint32_t)ST_MU, T, B, B_glob, b_off, A, mu);
+    if (act || rew || disc)
+        hipLaunchKernelGGL(synth_scalar_kernel, dim3(grid_for((size_t)T * B)), dim3(256), 0, s, seed,
+                           T, B, B_glob, b_off, A, gamma, act, rew, disc);
+    if (frames)
+        hipLaunchKernelGGL(synth_frames_kernel, dim3(grid_for((size_t)(T + 1) * B * 1764)), dim3(256),
+                           0, s, seed, T + 1, B, B_glob, b_off, (uint4*)frames);
+    FI_HIP_CHECK(hipGetLastError());
+    return FI_OK;
+}
+
+// ---------------------------------------------------------------- ingest
+// Record schema (one 1 KiB ELEMENT per step, reference data_structures.h:35, agent.h:62):
+//   [0,512) float obs[<=128] | [512,768) float mu_logits[<=64] | 768 int32 action |
+//   772 float reward | 776 float discount | 780 uint32 flags | 784.. reserved.
+// An entry holds T+1 records (record T = bootstrap observation).
+constexpr int REC_OBS = 0, REC_MU = 512, REC_ACT = 768, REC_REW = 772, REC_DISC = 776;
+
+__global__ void ingest_vec_kernel(const char* __restrict__ rec, int rows, int B, int W,
+                                  int rec_off, size_t entry_bytes, float* __restrict__ out) {
+    const size_t n = (size_t)rows * B * W;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const size_t lrow = i / W;
+        const int d = (int)(i - lrow * W);
+        const int t = (int)(lrow / B), b = (int)(lrow - (size_t)t * B);
+        out[i] = *(const float*)(rec + (size_t)b * entry_bytes + (size_t)t * FI_RECORD_BYTES +
+                                 rec_off + d * 4);
+    }
+}
+
+__global__ void ingest_scalar_kernel(const char* __restrict__ rec, int T, int B, int A,
+                                     size_t entry_bytes, int32_t* act, float* rew, float* disc) {
+    const size_t n = (size_t)T * B;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const int t = (int)(i / B), b = (int)(i - (size_t)t * B);
+        const char* r = rec + (size_t)b * entry_bytes + (size_t)t * FI_RECORD_BYTES;
+        int32_t a = *(const int32_t*)(r + REC_ACT);
+        act[i] = a < 0 ? 0 : (a >= A ? A - 1 : a);
+        rew[i] = *(const float*)(r + REC_REW);
+        disc[i] = *(const float*)(r + REC_DISC);
+    }
+}
+
+int ingest_launch(const void* rec, int T, int B, int A, int D, size_t entry_bytes, float* obs,
+                  float* mu, int32_t* act, float* rew, float* disc, hipStream_t s) {
+    FI_REQUIRE(rec && T >= 1 && B >= 1 && A >= 1 && A <= 64 && D <= 128, "ingest: bad shape");
+    FI_REQUIRE(entry_bytes >= (size_t)(T + 1) * FI_RECORD_BYTES, "ingest: entry too small");
+    const char* r = (const char*)rec;
+    if (obs)
+        hipLaunchKernelGGL(ingest_vec_kernel, dim3(grid_for((size_t)(T + 1) * B * D)), dim3(256), 0, s,
+                           r, T + 1, B, D, REC_OBS, entry_bytes, obs);
+    if (mu)
+        hipLaunchKernelGGL(ingest_vec_kernel, dim3(grid_for((size_t)T * B * A)), dim3(256), 0, s, r, T,
+                           B, A, REC_MU, entry_bytes, mu);
+    if (act && rew && disc)
+        hipLaunchKernelGGL(ingest_scalar_kernel, dim3(grid_for((size_t)T * B)), dim3(256), 0, s, r, T,
+                           B, A, entry_bytes, act, rew, disc);
+    FI_HIP_CHECK(hipGetLastError());
+    return FI_OK;
+}
+
+// ---------------------------------------------------------------- reductions
+__global__ void colsum_kernel(const float* __restrict__ Y, int M, int N, int rows_per,
+                              float* __restrict__ slab) {
+    const int m0 = blockIdx.x * rows_per, m1 = min(M, m0 + rows_per);
+    for (int n = threadIdx.x; n < N; n += blockDim.x) {
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+        int m = m0;
+        for (; m + 3 < m1; m += 4) {
+            s0 += Y[(size_t)m * N + n];
+            s1 += Y[(size_t)(m + 1) * N + n];
+            s2 += Y[(size_t)(m + 2) * N + n];
+            s3 += Y[(size_t)(m + 3) * N + n];
+        }
+        for (; m < m1; ++m) s0 += Y[(size_t)m * N + n];
+        slab[(size_t)blockIdx.x * N + n] = (s0 + s1) + (s2 + s3);
+    }
+}
+
+__global__ void heads_colsum_kernel(HeadsGrad g, int rows_per, float* __restrict__ slab) {
+    const int N = g.A + 1;
+    const int m0 = blockIdx.x * rows_per, m1 = min(g.rows, m0 + rows_per);
+    for (int n = threadIdx.x; n < N; n += blockDim.x) {
+        float s = 0.f;
+        for (int m = m0; m < m1; ++m) {
+            if (n < g.A) s += m < g.TB ? g.dlog[(size_t)m * g.A + n] : 0.f;
+            else s += g.dval[m];
+        }
+        slab[(size_t)blockIdx.x * N + n] = s;
+    }
+}
+
+int colsum_partial(const float* Y, int M, int N, int splits, float* slab, hipStream_t s) {
+    const int rows_per = (M + splits - 1) / splits;
+    hipLaunchKernelGGL(colsum_kernel, dim3(splits), dim3(256), 0, s, Y, M, N, rows_per, slab);
+    FI_HIP_CHECK(hipGetLastError());
+    return FI_OK;
+}
+
+int heads_colsum_partial(const HeadsGrad& g, int splits, float* slab, hipStream_t s) {
+    const int rows_per = (g.rows + splits - 1) / splits;
+    hipLaunchKernelGGL(heads_colsum_kernel, dim3(splits), dim3(64), 0, s, g, rows_per, slab);
+    FI_HIP_CHECK(hipGetLastError());
+    return FI_OK;
+}
+
+__global__ void reduce_slabs_kernel(const float* __restrict__ slab, int splits, size_t count,
+                                    float* __restrict__ out) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < count;
+         i += (size_t)gridDim.x * blockDim.x) {
+        float s = 0.f;
+        for (int k = 0; k < splits; ++k) s += slab[(size_t)k * count + i];
+        out[i] = s;
+    }
+}
+
+int reduce_slabs(const float* slab, int splits, size_t count, float* out, hipStream_t s) {
+    hipLaunchKernelGGL(reduce_slabs_kernel, dim3(grid_for(count)), dim3(256), 0, s, slab, splits,
+                       count, out);
+    FI_HIP_CHECK(hipGetLastError());
+    return FI_OK;
+}
+
+__global__ void sqnorm_part_kernel(const float* __restrict__ g, size_t n, double* part) {
+    __shared__ double red[4];
+    double s = 0.0;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x)
+        s += (double)g[i] * (double)g[i];
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ void sqnorm_final_kernel(const double* part, int nblk, double* out) {
+    __shared__ double red[4];
+    double s = 0.0;
+    for (int i = threadIdx.x; i < nblk; i += blockDim.x) s += part[i];
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) *out = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+int grad_sqnorm(const float* g, size_t n, double* part, int nblk, double* out, hipStream_t s) {
+    hipLaunchKernelGGL(sqnorm_part_kernel, dim3(nblk), dim3(256), 0, s, g, n, part);
+    hipLaunchKernelGGL(sqnorm_final_kernel, dim3(1), dim3(256), 0, s, part, nblk, out);
+    FI_HIP_CHECK(hipGetLastError());
+    return FI_OK;
+}
+
+// ---------------------------------------------------------------- optimizer
+__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                            float* __restrict__ m, float* __restrict__ v, size_t n, float lr,
+                            float b1, float b2, float eps, double bc1, double bc2,
+                            const double* sqnorm, float max_norm) {
+    float scale = 1.f;
+    if (max_norm > 0.f) {
+        const double norm = sqrt(*sqnorm);
+        if (norm > max_norm) scale = (float)((double)max_norm / (norm + 1e-6));
+    }
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const float gi = g[i] * scale;
+        const float mi = b1 * m[i] + (1.0f - b1) * gi;
+        const float vi = b2 * v[i] + (1.0f - b2) * gi * gi;
+        m[i] = mi;
+        v[i] = vi;
+        const double mh = mi / bc1, vh = vi / bc2;
+        p[i] = (float)(p[i] - lr * mh / (sqrt(vh) + eps));
+    }
+}
+
+__global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, size_t n, float lr,
+                           const double* sqnorm, float max_norm) {
+    float scale = 1.f;
+    if (max_norm > 0.f) {
+        const double norm = sqrt(*sqnorm);
+        if (norm > max_norm) scale = (float)((double)max_norm / (norm + 1e-6));
+    }
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x)
+        p[i] -= lr * (g[i] * scale);
+}
+
+int optimizer_step(int opt, float* p, const float* g, float* m, float* v, size_t n, float lr,
+                   float b1, float b2, float eps, double bc1, double bc2, const double* sqnorm,
+                   float max_norm, hipStream_t s) {
+    if (opt == FI_OPT_ADAM)
+        hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, s, p, g, m, v, n, lr, b1,
+                           b2, eps, bc1, bc2, sqnorm, max_norm);
+    else
+        hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n)), dim3(256), 0, s, p, g, n, lr, sqnorm,
+                           max_norm);
+    FI_HIP_CHECK(hipGetLastError());
+    return FI_OK;
+}
+
+__global__ void to_bf16_kernel(const float* __restrict__ src, uint16_t* __restrict__ dst, size_t n) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const __bf16 h = (__bf16)src[i];  // RNE (v_cvt_pk_bf16_f32)
+        dst[i] = __builtin_bit_cast(uint16_t, h);
+    }
+}
+
+int to_bf16(const float* src, uint16_t* dst, size_t n, hipStream_t s) {
+    hipLaunchKernelGGL(to_bf16_kernel, dim3(grid_for(n)), dim3(256), 0, s, src, dst, n);
+    FI_HIP_CHECK(hipGetLastError());
+    return FI_OK;
+}
+
+}  // namespace fi
+
+extern "C" int fi_synth_trajectories(uint64_t seed, int T, int B, int B_glob, int b_off, int A,
+                                     int D, float gamma, float* obs, float* mu, int32_t* act,
+                                     float* rew, float* disc, uint8_t* frames, void* stream) {
+    return fi::synth_launch(seed, T, B, B_glob, b_off, A, D, gamma, obs, mu, act, rew, disc, frames,
+                            (hipStream_t)stream);
+}
+
+extern "C" int fi_ingest_records(const void* rec, int T, int B, int A, int D, size_t entry_bytes,
+                                 float* obs, float* mu, int32_t* act, float* rew, float* disc,
+                                 void* stream) {
+    return fi::ingest_launch(rec, T, B, A, D, entry_bytes, obs, mu, act, rew, disc,
+                             (hipStream_t)stream);
+}

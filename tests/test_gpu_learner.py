@@ -1,0 +1,161 @@
+"""GPU parity of the whole MLP learner step (config #2 shape) against the CPU oracle.
+
+forward (fp32 MFMA) -> V-trace/loss -> backward -> optimizer, all through the C ABI
+(libfi_learner.so). Tolerance for fp32 tensors: max|d| <= 1e-5 * max(1, max|ref|) per tensor.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def scaled_close(a, b, tol=1e-5, what=""):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    assert np.isfinite(a).all(), what
+    s = max(1.0, float(np.abs(b).max()))
+    err = float(np.abs(a - b).max()) / s
+    assert err <= tol, f"{what}: scaled err {err:.3e}"
+
+
+def mk(T=5, B=16, A=18, D=128, H=256, **kw):
+    from freeimpala_amd.learner import DeviceLearner
+    kw.setdefault("optimizer", "sgd")
+    kw.setdefault("lr", 1e-3)
+    kw.setdefault("max_grad_norm", 0.0)
+    return DeviceLearner("mlp", seq_len=T, batch=B, num_actions=A, obs_dim=D, hidden=H, **kw)
+
+
+def oracle_step(orc, L, batch, p0):
+    T, B, A, D, H = L.T, L.B, L.A, L.D, L.H
+    obs = batch["obs"].reshape((T + 1) * B, D)
+    h1, h2, out = orc.mlp_forward(obs, p0, H=H, A=A)
+    logits = out[:, :A].reshape(T + 1, B, A)
+    values = out[:, A].reshape(T + 1, B)
+    vt = orc.vtrace_loss(logits[:T], batch["mu"], batch["actions"], batch["rewards"],
+                         batch["discounts"], values)
+    dout = np.zeros(((T + 1) * B, A + 1), np.float32)
+    dout[:T * B, :A] = vt["dlogits"].reshape(T * B, A)
+    dout[:, A] = vt["dvalue"].reshape(-1)
+    g = orc.mlp_backward(obs, p0, h1, h2, dout, H=H, A=A)
+    return dict(logits=logits, values=values, vt=vt, grads=g)
+
+
+def test_synth_bit_exact_vs_oracle(orc):
+    L = mk(T=6, B=16, D=32, H=32)
+    L.synth(seed=1234, b_global=64, b_offset=16)
+    ref = orc.synth_batch(1234, T=6, B=16, A=18, D=32, B_glob=64, b_off=16)
+    np.testing.assert_array_equal(L.tensor("obs", shape=(7, 16, 32)), ref["obs"])
+    np.testing.assert_array_equal(L.tensor("mu", shape=(6, 16, 18)), ref["mu"])
+    np.testing.assert_array_equal(L.tensor("actions", np.int32, (6, 16)), ref["actions"])
+    np.testing.assert_array_equal(L.tensor("rewards", shape=(6, 16)), ref["rewards"])
+    np.testing.assert_array_equal(L.tensor("discounts", shape=(6, 16)), ref["discounts"])
+
+
+@pytest.mark.parametrize("T,B", [(5, 16), (20, 48)])
+def test_mlp_step_parity(orc, T, B):
+    L = mk(T=T, B=B)
+    L.synth(seed=7)
+    batch = orc.synth_batch(7, T=T, B=B, A=18, D=128)
+    p0 = L.get_params()
+    st = L.step_resident()
+    ref = oracle_step(orc, L, batch, p0)
+    scaled_close(L.tensor("logits", shape=(T + 1, B, 18)), ref["logits"], what="logits")
+    scaled_close(L.tensor("values", shape=(T + 1, B)), ref["values"], what="values")
+    scaled_close(L.tensor("vs", shape=(T, B)), ref["vt"]["vs"], what="vs")
+    scaled_close(L.tensor("dlogits", shape=(T, B, 18)), ref["vt"]["dlogits"], what="dlogits")
+    g = L.tensor("grads")
+    D, H, A = 128, 256, 18
+    off = np.cumsum([0, D * H, H, H * H, H, H * (A + 1), A + 1])
+    for i, name in enumerate(["W1", "b1", "W2", "b2", "Wh", "bh"]):
+        scaled_close(g[off[i]:off[i + 1]], ref["grads"][off[i]:off[i + 1]], what=name)
+    tot = ref["vt"]["losses"]
+    assert abs(st["pg_loss"] - tot[0]) <= 1e-5 * max(1, abs(tot[0]))
+    assert abs(st["baseline_loss"] - tot[1]) <= 1e-5 * max(1, abs(tot[1]))
+    assert abs(st["entropy_loss"] - tot[2]) <= 1e-5 * max(1, abs(tot[2]))
+    np.testing.assert_allclose(st["grad_norm"], np.linalg.norm(ref["grads"].astype(np.float64)),
+                               rtol=1e-5)
+    # SGD, no clipping: p1 = p0 - lr * g
+    scaled_close(L.get_params(), p0 - np.float32(1e-3) * g, 1e-6, "sgd update")
+    assert st["version"] == 1
+
+
+def test_mlp_config2_full_size(orc):
+    """Config #2: T=100, B=512, A=18, obs 128, MLP 128-256-256, fp32 numerics vs the oracle."""
+    T, B = 100, 512
+    L = mk(T=T, B=B)
+    L.synth(seed=42)
+    batch = orc.synth_batch(42, T=T, B=B, A=18, D=128)
+    p0 = L.get_params()
+    L.step_resident()
+    ref = oracle_step(orc, L, batch, p0)
+    scaled_close(L.tensor("vs", shape=(T, B)), ref["vt"]["vs"], what="vs")
+    scaled_close(L.tensor("pg_adv", shape=(T, B)), ref["vt"]["pg_adv"], what="pg_adv")
+    scaled_close(L.tensor("dlogits", shape=(T, B, 18)), ref["vt"]["dlogits"], what="dlogits")
+    scaled_close(L.tensor("dvalue", shape=(T + 1, B)), ref["vt"]["dvalue"], what="dvalue")
+    scaled_close(L.tensor("grads"), ref["grads"], 2e-5, what="grads")
+
+
+def test_adam_and_clip_match_oracle(orc):
+    L = mk(T=4, B=16, optimizer="adam", lr=5e-4, max_grad_norm=1.0)
+    L.synth(seed=3)
+    p0 = L.get_params()
+    st = L.step_resident()
+    g = L.tensor("grads")
+    p = p0.copy()
+    gg = g.copy()
+    norm = orc.clip_grad_norm(gg, 1.0)
+    np.testing.assert_allclose(st["grad_norm"], norm, rtol=1e-6)
+    m = np.zeros_like(p)
+    v = np.zeros_like(p)
+    orc.adam(p, gg, m, v, 5e-4, 0.9, 0.999, 1e-8, 1)
+    scaled_close(L.get_params(), p, 1e-6, "adam params")
+    scaled_close(L.tensor("adam_m"), m, 1e-6, "adam m")
+
+
+def test_host_entries_step_equals_resident_step(orc):
+    """SharedBuffer entries (host bytes, record schema) -> ingest kernel -> same step."""
+    from freeimpala_amd.learner import pack_records
+    T, B = 8, 32
+    batch = orc.synth_batch(11, T=T, B=B, A=18, D=128)
+    entries = pack_records(batch["obs"], batch["mu"], batch["actions"], batch["rewards"],
+                           batch["discounts"], entry_size=T + 3)
+    L1, L2 = mk(T=T, B=B, seed=5), mk(T=T, B=B, seed=5)
+    L1.synth(seed=11)
+    s1 = L1.step_resident()
+    s2 = L2.step(entries)
+    np.testing.assert_array_equal(L2.tensor("obs"), L1.tensor("obs"))
+    np.testing.assert_array_equal(L2.tensor("actions", np.int32), L1.tensor("actions", np.int32))
+    np.testing.assert_array_equal(L2.get_params(), L1.get_params())
+    assert s1["total_loss"] == s2["total_loss"]
+
+
+def test_publish_blob_and_resume():
+    L = mk(T=3, B=16, publish="bf16")
+    assert L.param_bytes == 2 * L.param_count
+    L.synth(seed=1)
+    L.step_resident()
+    blob, ver = L.get_blob()
+    assert ver == 1 and len(blob) == L.param_bytes
+    L2 = mk(T=3, B=16, seed=99)
+    L2.set_params(blob, version=ver)
+    p1 = L.get_params()
+    p2 = L2.get_params()
+    # bf16 round trip: |d| <= 2^-8 relative
+    assert np.all(np.abs(p2 - p1) <= np.abs(p1) * 2 ** -8 + 1e-30)
+
+
+def test_loss_decreases_over_steps():
+    L = mk(T=10, B=64, optimizer="adam", lr=1e-3, max_grad_norm=40.0)
+    L.synth(seed=5)
+    losses = [L.step_resident()["total_loss"] for _ in range(30)]
+    assert losses[-1] < losses[0]
+
+
+def test_bad_arguments_fail_loudly():
+    from freeimpala_amd._abi import FiError
+    L = mk(T=3, B=16)
+    with pytest.raises(FiError):
+        L.step([b"\0" * 1024] * 16)  # entries shorter than (T+1)*1024
+    with pytest.raises(FiError):
+        L.step([b"\0" * 4096] * 15)  # wrong batch size
