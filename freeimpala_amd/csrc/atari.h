@@ -8,6 +8,22 @@
 
 namespace fi {
 
+// per-launch timing hook (implemented by the learner's profiling events)
+struct KernelTagger {
+    virtual void begin(const char* name) = 0;
+    virtual void end() = 0;
+    virtual ~KernelTagger() {}
+};
+struct TagScope {
+    KernelTagger* t;
+    TagScope(KernelTagger* t_, const char* name) : t(t_) {
+        if (t) t->begin(name);
+    }
+    ~TagScope() {
+        if (t) t->end();
+    }
+};
+
 struct AtariNet {
     static constexpr size_t kFrameBytes = 84 * 84 * 4;
     int B = 0, T = 0, A = 0, N = 0;  // N = (T+1)*B frames
@@ -19,9 +35,10 @@ void atari_init_params(int A, uint64_t seed, std::vector<float>& p);
 AtariNet* atari_create(int B, int T, int A);
 void atari_destroy(AtariNet* n);
 int atari_sync_weights(AtariNet* n, const float* params, hipStream_t s);
-int atari_forward(AtariNet* n, const uint8_t* frames, float* logits, float* values, hipStream_t s);
+int atari_forward(AtariNet* n, const uint8_t* frames, float* logits, float* values, hipStream_t s,
+                  KernelTagger* tg = nullptr);
 int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, const float* dvalue,
-                   float* grads, hipStream_t s);
+                   float* grads, hipStream_t s, KernelTagger* tg = nullptr);
 bool atari_tensor(AtariNet* n, const char* name, void** p, size_t* bytes);
 
 }  // namespace fi

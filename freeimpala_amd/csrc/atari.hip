@@ -1,22 +1,690 @@
-// atari.hip -- placeholder until the bf16 conv path lands (returns FI_ERR_UNSUPPORTED).
+// atari.hip -- the Atari-shaped conv policy of config #3 on bf16 MFMA (gfx950).
+//
+// No reference counterpart: the reference learner has no network (learner.h:32-49). The
+// architecture is the SURVEY.md 8(a) "Policy network" row (Nature-DQN torso as used by
+// IMPALA/torchbeast): frames u8 (84,84,4)/255 -> conv 8x8/4 32 -> conv 4x4/2 64 ->
+// conv 3x3/1 64 -> fc 3136->512 -> heads (A logits | value). NHWC everywhere, activations
+// and upstream gradients in bf16, fp32 accumulation, fp32 master weights / grads / Adam.
+//
+// Every layer is one of two MFMA (v_mfma_f32_32x32x16_bf16) kernels:
+//  * bf16_gemm  -- C[m][n] = sum_k A(m,k) B(n,k): forward convs as implicit GEMM (A gathered
+//    from the NHWC input 16 bytes = 8 channels at a time; conv1 gathers 8 u8 = 2 pixels x 4
+//    channels), fc/heads, and data-gradients (dgrad of a strided conv is split into S*S
+//    parity classes so every M-tile uses one weight slice). Both operands are staged through
+//    padded LDS rows (80 B: conflict-free ds_read_b128 fragment reads), register prefetch of
+//    the next K-tile overlaps the MFMAs. Epilogues fuse bias + ReLU (+1/255 scale), the
+//    heads split, and the ReLU mask of the backward pass.
+//  * bf16_wgrad -- weight gradients C[i][j] = sum_m A(m,i) B(m,j): the reduction runs over
+//    output pixels, so tiles are staged [m][i] and fed to the MFMA with the gfx950 transpose
+//    read ds_read_b64_tr_b16 (no shuffles); split over m into fp32 slabs reduced in a fixed
+//    order (deterministic); the bias gradient (column sums of B) rides along.
+#include <vector>
+
 #include "atari.h"
 #include "fi_common.h"
+#include "kernels.h"
 
 namespace fi {
-size_t atari_param_count(int A) {
-    return 8 * 8 * 4 * 32 + 32 + 4 * 4 * 32 * 64 + 64 + 3 * 3 * 64 * 64 + 64 + (size_t)3136 * 512 +
-           512 + (size_t)512 * (A + 1) + (A + 1);
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------ geometry
+namespace geo {
+constexpr int C1K = 256, C1O = 32;           // conv1: k = (ky,kx,ci) 8*8*4
+constexpr int C2K = 512, C2O = 64;           // conv2: 4*4*32
+constexpr int C3K = 576, C3O = 64;           // conv3: 3*3*64
+constexpr int FCK = 3136, FCO = 512;         // fc
+constexpr int HP = 32;                       // heads padded output width (A+1 <= 32)
+constexpr int P1 = 400, P2 = 81, P3 = 49;    // output pixels per frame
+}  // namespace geo
+
+struct Offsets {  // offsets into the fp32 parameter blob (== oracle layout)
+    size_t c1w, c1b, c2w, c2b, c3w, c3b, fcw, fcb, hw, hb, total;
+    explicit Offsets(int A) {
+        size_t o = 0;
+        c1w = o; o += 8 * 8 * 4 * 32; c1b = o; o += 32;
+        c2w = o; o += 4 * 4 * 32 * 64; c2b = o; o += 64;
+        c3w = o; o += 3 * 3 * 64 * 64; c3b = o; o += 64;
+        fcw = o; o += (size_t)3136 * 512; fcb = o; o += 512;
+        hw = o; o += (size_t)512 * (A + 1); hb = o; o += A + 1;
+        total = o;
+    }
+};
+
+size_t atari_param_count(int A) { return Offsets(A).total; }
+
+void atari_init_params(int A, uint64_t seed, std::vector<float>& p) {
+    // Glorot-uniform (fan_in = kh*kw*cin, fan_out = kh*kw*cout), zero biases.
+    Offsets off(A);
+    p.assign(off.total, 0.f);
+    uint64_t st = seed ^ 0xA7A21ull;
+    auto next = [&]() {
+        uint64_t z = (st += 0x9E3779B97F4A7C15ull);
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return z ^ (z >> 31);
+    };
+    auto fill = [&](size_t o, size_t n, double fi, double fo) {
+        const double lim = std::sqrt(6.0 / (fi + fo));
+        for (size_t i = 0; i < n; ++i) {
+            const double u = (double)(next() >> 11) * (1.0 / 9007199254740992.0);
+            p[o + i] = (float)((2.0 * u - 1.0) * lim);
+        }
+    };
+    fill(off.c1w, 8192, 256, 64 * 32);
+    fill(off.c2w, 32768, 512, 16 * 64);
+    fill(off.c3w, 36864, 576, 9 * 64);
+    fill(off.fcw, (size_t)3136 * 512, 3136, 512);
+    fill(off.hw, (size_t)512 * (A + 1), 512, A + 1);
 }
-void atari_init_params(int A, uint64_t, std::vector<float>& p) { p.assign(atari_param_count(A), 0.f); }
-AtariNet* atari_create(int, int, int) {
-    set_error("Atari conv policy not built yet");
-    return nullptr;
+
+// ------------------------------------------------------------------ operand loaders
+// Each returns 8 consecutive k (or i) values of row r as 8 packed bf16 (16 bytes), zero
+// outside the matrix. kc = k / 8.
+__device__ __forceinline__ u32x4 zero4() { return u32x4{0u, 0u, 0u, 0u}; }
+
+struct RowsBf16 {  // plain row-major bf16 matrix [rows][ld]
+    const __bf16* p;
+    int rows, ld;
+    __device__ void set_tile(int) {}
+    __device__ u32x4 load(int r, int kc) const {
+        if (r >= rows || kc * 8 >= ld) return zero4();
+        return *(const u32x4*)(p + (size_t)r * ld + kc * 8);
+    }
+};
+
+// conv1 input: frames u8 [N][84][84][4]; k = (ky*8 + kx)*4 + c, a k-chunk = 2 pixels x 4 ch
+struct Conv1Gather {
+    const uint8_t* fr;
+    int rows;  // N*400
+    __device__ void set_tile(int) {}
+    __device__ u32x4 load(int m, int kc) const {
+        if (m >= rows) return zero4();
+        const int n = m / 400, pix = m - n * 400;
+        const int oy = pix / 20, ox = pix - oy * 20;
+        const int ky = kc >> 2, kx = (kc & 3) * 2;
+        const uint2 v = *(const uint2*)(fr + (((size_t)n * 84 + oy * 4 + ky) * 84 + ox * 4 + kx) * 4);
+        bf16x8 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            o[j] = (__bf16)(float)((v.x >> (8 * j)) & 0xffu);
+            o[4 + j] = (__bf16)(float)((v.y >> (8 * j)) & 0xffu);
+        }
+        return __builtin_bit_cast(u32x4, o);
+    }
+};
+
+// NHWC bf16 conv input, kernel KS, stride S, channels C (multiple of 8), output OH x OH
+template <int H, int C, int KS, int S, int OH>
+struct ConvGather {
+    const __bf16* x;
+    int rows;  // N * OH * OH
+    __device__ void set_tile(int) {}
+    __device__ u32x4 load(int m, int kc) const {
+        if (m >= rows || kc * 8 >= KS * KS * C) return zero4();
+        const int n = m / (OH * OH), pix = m - n * (OH * OH);
+        const int oy = pix / OH, ox = pix - oy * OH;
+        const int k = kc * 8;
+        const int ky = k / (KS * C), kx = (k / C) % KS, c = k % C;
+        return *(const u32x4*)(x + (((size_t)n * H + oy * S + ky) * H + ox * S + kx) * C + c);
+    }
+};
+
+// dgrad of a conv (kernel KS, stride S, in IH x IH x Ci, out OH x OH x Co): rows are input
+// pixels grouped by parity class (py,px); a class occupies `cstride` rows (>= N*Q*Q, padded
+// to the M-tile) with Q = IH / S. k = (ty, tx, co), ky = py + S*ty, oy = iy' - ty.
+template <int IH, int KS, int S, int OH, int CO>
+struct DgradGather {
+    const __bf16* dy;  // [N][OH][OH][CO]
+    int nf, cstride;
+    static constexpr int Q = IH / S, TT = KS / S;
+    __device__ void set_tile(int) {}
+    __device__ u32x4 load(int m, int kc) const {
+        const int cls = m / cstride, r = m - cls * cstride;
+        if (cls >= S * S || r >= nf * Q * Q) return zero4();
+        const int n = r / (Q * Q), q2 = r - n * (Q * Q);
+        const int iyq = q2 / Q, ixq = q2 - iyq * Q;
+        const int k = kc * 8;
+        const int tap = k / CO, co = k - tap * CO;
+        if (tap >= TT * TT) return zero4();
+        const int ty = tap / TT, tx = tap - ty * TT;
+        const int oy = iyq - ty, ox = ixq - tx;
+        if (oy < 0 || oy >= OH || ox < 0 || ox >= OH) return zero4();
+        return *(const u32x4*)(dy + (((size_t)n * OH + oy) * OH + ox) * CO + co);
+    }
+};
+
+// dgrad weights for parity class of the current M-tile: [cls][ci][k]
+struct ClassRows {
+    const __bf16* p;
+    int rows, ld, cstride;
+    size_t cls_stride;
+    const __bf16* cur;
+    __device__ void set_tile(int m0) { cur = p + (size_t)(m0 / cstride) * cls_stride; }
+    __device__ u32x4 load(int r, int kc) const {
+        if (r >= rows || kc * 8 >= ld) return zero4();
+        return *(const u32x4*)(cur + (size_t)r * ld + kc * 8);
+    }
+};
+
+// the heads' upstream gradient [rows][32]: dlogits (fp32, TB rows) | dvalue | 0 -> bf16
+struct DoutRows {
+    const float* dlog;
+    const float* dval;
+    int rows, TB, A;
+    __device__ void set_tile(int) {}
+    __device__ u32x4 load(int m, int kc) const {
+        if (m >= rows) return zero4();
+        bf16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int c = kc * 8 + j;
+            float v = 0.f;
+            if (c < A) v = m < TB ? dlog[(size_t)m * A + c] : 0.f;
+            else if (c == A) v = dval[m];
+            o[j] = (__bf16)v;
+        }
+        return __builtin_bit_cast(u32x4, o);
+    }
+};
+
+// ------------------------------------------------------------------ epilogues
+struct EpiAct {  // out[m][n] = bf16(relu(acc*scale + bias[n]))
+    __bf16* out;
+    int ld;
+    const float* bias;
+    float scale;
+    __device__ void operator()(int m, int n, float v) const {
+        v = fmaxf(v * scale + bias[n], 0.f);
+        out[(size_t)m * ld + n] = (__bf16)v;
+    }
+};
+struct EpiHeadsOut {
+    float* logits;
+    float* values;
+    const float* bias;
+    int A;
+    __device__ void operator()(int m, int n, float v) const {
+        if (n > A) return;
+        v += bias[n];
+        if (n < A) logits[(size_t)m * A + n] = v;
+        else values[m] = v;
+    }
+};
+struct EpiMaskBf16 {  // out[m][n] = bf16(acc) if act[m][n] > 0 else 0
+    __bf16* out;
+    const __bf16* act;
+    int ld;
+    __device__ void operator()(int m, int n, float v) const {
+        const size_t i = (size_t)m * ld + n;
+        out[i] = (float)act[i] > 0.f ? (__bf16)v : (__bf16)0.f;
+    }
+};
+template <int IH, int S>
+struct EpiDgrad {  // class-ordered row -> input pixel; masked by the input activation
+    __bf16* out;
+    const __bf16* act;
+    int nf, cstride, ci;
+    static constexpr int Q = IH / S;
+    __device__ void operator()(int m, int n, float v) const {
+        const int cls = m / cstride, r = m - cls * cstride;
+        if (r >= nf * Q * Q) return;
+        const int b = r / (Q * Q), q2 = r - b * (Q * Q);
+        const int iy = (q2 / Q) * S + cls / S, ix = (q2 % Q) * S + cls % S;
+        const size_t i = (((size_t)b * IH + iy) * IH + ix) * ci + n;
+        out[i] = (float)act[i] > 0.f ? (__bf16)v : (__bf16)0.f;
+    }
+};
+
+// ------------------------------------------------------------------ bf16_gemm
+constexpr int KB = 32;         // k per LDS stage
+constexpr int LROW = KB + 8;   // padded LDS row (bf16): 80 bytes
+
+template <int BM, int BN, int WM, int WN, class LA, class LB, class Epi>
+__global__ __launch_bounds__(256) void bf16_gemm(LA la, LB lb, Epi epi, int M, int N, int K) {
+    constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+    constexpr int CA = BM * (KB / 8) / 256;  // 16-byte chunks per thread
+    constexpr int CBT = BN * (KB / 8);
+    constexpr int CB = (CBT + 255) / 256;
+    static_assert(TM >= 1 && TN >= 1 && WM * WN == 4 && CA >= 1, "tile");
+    __shared__ __attribute__((aligned(16))) __bf16 sA[2][BM * LROW];
+    __shared__ __attribute__((aligned(16))) __bf16 sB[2][BN * LROW];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w / WN, wn = w % WN;
+    const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+    la.set_tile(m0);
+    lb.set_tile(m0);
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
+    u32x4 ra[CA], rb[CB];
+    auto fetch = [&](int kc0) {
+#pragma unroll
+        for (int i = 0; i < CA; ++i) {
+            const int idx = tid + 256 * i;
+            ra[i] = la.load(m0 + (idx >> 2), kc0 + (idx & 3));
+        }
+#pragma unroll
+        for (int i = 0; i < CB; ++i) {
+            const int idx = tid + 256 * i;
+            if (idx < CBT) rb[i] = lb.load(n0 + (idx >> 2), kc0 + (idx & 3));
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < CA; ++i) {
+            const int idx = tid + 256 * i;
+            *(u32x4*)&sA[buf][(idx >> 2) * LROW + (idx & 3) * 8] = ra[i];
+        }
+#pragma unroll
+        for (int i = 0; i < CB; ++i) {
+            const int idx = tid + 256 * i;
+            if (idx < CBT) *(u32x4*)&sB[buf][(idx >> 2) * LROW + (idx & 3) * 8] = rb[i];
+        }
+    };
+    const int nk = (K + KB - 1) / KB;
+    fetch(0);
+    store(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        const int buf = kt & 1;
+        if (kt + 1 < nk) fetch((kt + 1) * (KB / 8));
+#pragma unroll
+        for (int ks = 0; ks < KB / 16; ++ks) {
+            bf16x8 af[TM], bfv[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+                af[i] = *(const bf16x8*)&sA[buf][(wm * (BM / WM) + i * 32 + (lane & 31)) * LROW + ks * 16 +
+                                                 (lane >> 5) * 8];
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+                bfv[j] = *(const bf16x8*)&sB[buf][(wn * (BN / WN) + j * 32 + (lane & 31)) * LROW + ks * 16 +
+                                                  (lane >> 5) * 8];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
+        }
+        if (kt + 1 < nk) store(buf ^ 1);
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                const int n = n0 + wn * (BN / WN) + j * 32 + (lane & 31);
+                if (m < M && n < N) epi(m, n, acc[i][j][r]);
+            }
 }
-void atari_destroy(AtariNet* n) { delete n; }
-int atari_sync_weights(AtariNet*, const float*, hipStream_t) { return fail(FI_ERR_UNSUPPORTED, "atari"); }
-int atari_forward(AtariNet*, const uint8_t*, float*, float*, hipStream_t) { return fail(FI_ERR_UNSUPPORTED, "atari"); }
-int atari_backward(AtariNet*, const uint8_t*, const float*, const float*, float*, hipStream_t) {
-    return fail(FI_ERR_UNSUPPORTED, "atari");
+
+template <int BM, int BN, int WM, int WN, class LA, class LB, class Epi>
+static int gemm(LA la, LB lb, Epi epi, int M, int N, int K, hipStream_t s) {
+    dim3 grid((M + BM - 1) / BM, (N + BN - 1) / BN);
+    hipLaunchKernelGGL((bf16_gemm<BM, BN, WM, WN, LA, LB, Epi>), grid, dim3(256), 0, s, la, lb, epi, M,
+                       N, K);
+    FI_HIP_CHECK(hipGetLastError());
+    return FI_OK;
 }
-bool atari_tensor(AtariNet*, const char*, void**, size_t*) { return false; }
+
+// ------------------------------------------------------------------ bf16_wgrad
+// C[i][j] = scale * sum_m A(m, i) B(m, j) for m in [split*mps, (split+1)*mps)
+// LDS rows are m; pitch chosen so the transposed b64 reads are bank-conflict free.
+constexpr int MC = 32;  // m per LDS stage (2 MFMA K-steps)
+template <int W>
+struct TrPitch {
+    static constexpr int value = (W % 128 == 0) ? W + 32 : (W % 64 == 0 ? W + 32 : W);
+};
+
+__device__ __forceinline__ bf16x8 tr_frag(const __bf16* base, int pitch, int lane) {
+    // operand fragment of a 32x32x16 MFMA whose K index runs down the LDS rows:
+    // lane l gets column (l&15) + 16*((l>>4)&1) of rows 8*(l>>5) + 0..7
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const __bf16* a0 = base + (8 * (g >> 1) + q) * pitch + 16 * (g & 1) + 4 * p;
+    typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a0));
+    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a0 + 4 * pitch));
+    return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+template <int BI, int BJ, int WI, int WJ, class LA, class LB>
+__global__ __launch_bounds__(256) void bf16_wgrad(LA la, LB lb, float* __restrict__ slab,
+                                                  float* __restrict__ cs_slab, int M, int I, int J,
+                                                  int mps, float scale) {
+    constexpr int TI = BI / WI / 32, TJ = BJ / WJ / 32;
+    constexpr int PA = TrPitch<BI>::value, PB = TrPitch<BJ>::value;
+    constexpr int CA = MC * (BI / 8) / 256, CBT = MC * (BJ / 8);
+    constexpr int CB = (CBT + 255) / 256;
+    static_assert(TI >= 1 && TJ >= 1 && WI * WJ == 4 && CA >= 1, "tile");
+    __shared__ __attribute__((aligned(16))) __bf16 sA[2][MC * PA];
+    __shared__ __attribute__((aligned(16))) __bf16 sB[2][MC * PB];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wi = w / WJ, wj = w % WJ;
+    const int i0 = blockIdx.x * BI, j0 = blockIdx.y * BJ;
+    const int mb = blockIdx.z * mps, me = min(M, mb + mps);
+    const bool do_cs = blockIdx.x == 0 && tid < BJ;
+    float cs = 0.f;
+    f32x16 acc[TI][TJ];
+#pragma unroll
+    for (int a = 0; a < TI; ++a)
+#pragma unroll
+        for (int b = 0; b < TJ; ++b) acc[a][b] = f32x16{};
+    u32x4 ra[CA], rb[CB];
+    constexpr int AQ = BI / 8, BQ = BJ / 8;  // 16-byte chunks per LDS row
+    auto fetch = [&](int mm) {
+#pragma unroll
+        for (int c = 0; c < CA; ++c) {
+            const int idx = tid + 256 * c;
+            const int r = idx / AQ, q = idx - r * AQ;
+            ra[c] = (mm + r < me) ? la.load(mm + r, i0 / 8 + q) : zero4();
+        }
+#pragma unroll
+        for (int c = 0; c < CB; ++c) {
+            const int idx = tid + 256 * c;
+            const int r = idx / BQ, q = idx - r * BQ;
+            if (idx < CBT) rb[c] = (mm + r < me) ? lb.load(mm + r, j0 / 8 + q) : zero4();
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int c = 0; c < CA; ++c) {
+            const int idx = tid + 256 * c;
+            const int r = idx / AQ, q = idx - r * AQ;
+            *(u32x4*)&sA[buf][r * PA + q * 8] = ra[c];
+        }
+#pragma unroll
+        for (int c = 0; c < CB; ++c) {
+            const int idx = tid + 256 * c;
+            const int r = idx / BQ, q = idx - r * BQ;
+            if (idx < CBT) *(u32x4*)&sB[buf][r * PB + q * 8] = rb[c];
+        }
+    };
+    if (mb < me) {
+        fetch(mb);
+        store(0);
+    }
+    __syncthreads();
+    int buf = 0;
+    for (int mm = mb; mm < me; mm += MC) {
+        const bool more = mm + MC < me;
+        if (more) fetch(mm + MC);
+#pragma unroll
+        for (int ks = 0; ks < MC / 16; ++ks) {
+            bf16x8 af[TI], bfv[TJ];
+#pragma unroll
+            for (int a = 0; a < TI; ++a)
+                af[a] = tr_frag(&sA[buf][ks * 16 * PA + wi * (BI / WI) + a * 32], PA, lane);
+#pragma unroll
+            for (int b = 0; b < TJ; ++b)
+                bfv[b] = tr_frag(&sB[buf][ks * 16 * PB + wj * (BJ / WJ) + b * 32], PB, lane);
+#pragma unroll
+            for (int a = 0; a < TI; ++a)
+#pragma unroll
+                for (int b = 0; b < TJ; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bfv[b], acc[a][b], 0, 0, 0);
+        }
+        if (do_cs) {
+#pragma unroll 8
+            for (int r = 0; r < MC; ++r) cs += (float)sB[buf][r * PB + tid];
+        }
+        if (more) store(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+    float* out = slab + (size_t)blockIdx.z * I * J;
+#pragma unroll
+    for (int a = 0; a < TI; ++a)
+#pragma unroll
+        for (int b = 0; b < TJ; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int i = i0 + wi * (BI / WI) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                const int j = j0 + wj * (BJ / WJ) + b * 32 + (lane & 31);
+                if (i < I && j < J) out[(size_t)i * J + j] = acc[a][b][r] * scale;
+            }
+    if (do_cs && j0 + tid < J) cs_slab[(size_t)blockIdx.z * J + j0 + tid] = cs;
+}
+
+template <int BI, int BJ, int WI, int WJ, class LA, class LB>
+static int wgrad(LA la, LB lb, float* slab, float* cs_slab, int M, int I, int J, int splits,
+                 float scale, hipStream_t s) {
+    const int mps = ((M + splits - 1) / splits + MC - 1) / MC * MC;
+    dim3 grid((I + BI - 1) / BI, (J + BJ - 1) / BJ, splits);
+    hipLaunchKernelGGL((bf16_wgrad<BI, BJ, WI, WJ, LA, LB>), grid, dim3(256), 0, s, la, lb, slab, cs_slab,
+                       M, I, J, mps, scale);
+    FI_HIP_CHECK(hipGetLastError());
+    return FI_OK;
+}
+
+// ------------------------------------------------------------------ weight layouts (bf16)
+struct WeightsBf16 {
+    __bf16 *c1T, *c2T, *c3T, *fcT, *hT;  // forward B operands [out][k]
+    __bf16 *c2D, *c3D, *fcB, *hD;        // dgrad B operands
+};
+
+__global__ void weights_bf16_kernel(const float* __restrict__ p, Offsets o, int A, WeightsBf16 w) {
+    const int O = A + 1;
+    // segment sizes
+    const size_t n1 = 32 * 256, n2 = 64 * 512, n3 = 64 * 576, nf = (size_t)512 * 3136,
+                 nh = 32 * 512, n2d = 4 * 32 * 256, n3d = 64 * 576, nfb = nf, nhd = 512 * 32;
+    const size_t total = n1 + n2 + n3 + nf + nh + n2d + n3d + nfb + nhd;
+    for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < total;
+         t += (size_t)gridDim.x * blockDim.x) {
+        size_t i = t;
+        if (i < n1) { const int co = i / 256, k = i % 256; w.c1T[i] = (__bf16)p[o.c1w + (size_t)k * 32 + co]; continue; }
+        i -= n1;
+        if (i < n2) { const int co = i / 512, k = i % 512; w.c2T[i] = (__bf16)p[o.c2w + (size_t)k * 64 + co]; continue; }
+        i -= n2;
+        if (i < n3) { const int co = i / 576, k = i % 576; w.c3T[i] = (__bf16)p[o.c3w + (size_t)k * 64 + co]; continue; }
+        i -= n3;
+        if (i < nf) { const size_t j = i / 3136, k = i % 3136; w.fcT[i] = (__bf16)p[o.fcw + k * 512 + j]; continue; }
+        i -= nf;
+        if (i < nh) { const int oo = i / 512, j = i % 512; w.hT[i] = (__bf16)(oo < O ? p[o.hw + (size_t)j * O + oo] : 0.f); continue; }
+        i -= nh;
+        if (i < n2d) {  // [cls][ci][(ty,tx,co)]
+            const int cls = i / (32 * 256), r = i % (32 * 256), ci = r / 256, k = r % 256;
+            const int tap = k / 64, co = k % 64, ty = tap / 2, tx = tap % 2;
+            const int ky = cls / 2 + 2 * ty, kx = cls % 2 + 2 * tx;
+            w.c2D[i] = (__bf16)p[o.c2w + (((size_t)ky * 4 + kx) * 32 + ci) * 64 + co];
+            continue;
+        }
+        i -= n2d;
+        if (i < n3d) {  // [ci][(ky,kx,co)]
+            const int ci = i / 576, k = i % 576, tap = k / 64, co = k % 64;
+            w.c3D[i] = (__bf16)p[o.c3w + ((size_t)tap * 64 + ci) * 64 + co];
+            continue;
+        }
+        i -= n3d;
+        if (i < nfb) { w.fcB[i] = (__bf16)p[o.fcw + i]; continue; }
+        i -= nfb;
+        { const int j = i / 32, oo = i % 32; w.hD[i] = (__bf16)(oo < O ? p[o.hw + (size_t)j * O + oo] : 0.f); }
+    }
+}
+
+// ------------------------------------------------------------------ the net
+struct AtariImpl {
+    int N = 0, A = 0, TB = 0;
+    Offsets off{18};
+    WeightsBf16 wb{};
+    __bf16 *a1 = nullptr, *a2 = nullptr, *a3 = nullptr, *h = nullptr;
+    __bf16 *da1 = nullptr, *da2 = nullptr, *da3 = nullptr, *dh = nullptr;
+    float* slab = nullptr;
+    size_t slab_floats = 0;
+    const float* params = nullptr;  // last synced fp32 params (for biases)
+    std::vector<void*> allocs;
+    int cs2 = 0, cs3 = 0;  // class strides for the dgrad GEMMs
+};
+
+static AtariImpl* impl(AtariNet* n) { return (AtariImpl*)n->impl; }
+
+template <typename T>
+static bool dmalloc(AtariImpl* I, T** p, size_t n) {
+    if (hipMalloc((void**)p, n * sizeof(T) + 16) != hipSuccess) {
+        *p = nullptr;
+        return false;
+    }
+    I->allocs.push_back(*p);
+    return true;
+}
+
+// split factors (blocks over the reduction) per weight-gradient GEMM
+constexpr int SPL_H = 128, SPL_FC = 8, SPL_C3 = 160, SPL_C2 = 256, SPL_C1 = 512;
+constexpr int GBM = 128;  // M-tile of the dgrad GEMMs (class stride granularity)
+
+AtariNet* atari_create(int B, int T, int A) {
+    if (A + 1 > geo::HP) {
+        set_error("atari: A+1 must be <= 32");
+        return nullptr;
+    }
+    AtariNet* n = new AtariNet();
+    AtariImpl* I = new AtariImpl();
+    n->impl = I;
+    n->B = B; n->T = T; n->A = A; n->N = (T + 1) * B;
+    I->N = n->N; I->A = A; I->TB = T * B; I->off = Offsets(A);
+    const size_t N = n->N;
+    I->cs2 = (int)(((N * 100) + GBM - 1) / GBM * GBM);
+    I->cs3 = (int)(((N * 81) + GBM - 1) / GBM * GBM);
+    bool ok = dmalloc(I, &I->a1, N * 400 * 32) && dmalloc(I, &I->a2, N * 81 * 64) &&
+              dmalloc(I, &I->a3, N * 3136) && dmalloc(I, &I->h, N * 512) &&
+              dmalloc(I, &I->da1, N * 400 * 32) && dmalloc(I, &I->da2, N * 81 * 64) &&
+              dmalloc(I, &I->da3, N * 3136) && dmalloc(I, &I->dh, N * 512) &&
+              dmalloc(I, &I->wb.c1T, 32 * 256) && dmalloc(I, &I->wb.c2T, 64 * 512) &&
+              dmalloc(I, &I->wb.c3T, 64 * 576) && dmalloc(I, &I->wb.fcT, (size_t)512 * 3136) &&
+              dmalloc(I, &I->wb.hT, 32 * 512) && dmalloc(I, &I->wb.c2D, 4 * 32 * 256) &&
+              dmalloc(I, &I->wb.c3D, 64 * 576) && dmalloc(I, &I->wb.fcB, (size_t)3136 * 512) &&
+              dmalloc(I, &I->wb.hD, 512 * 32);
+    const size_t s_fc = (size_t)SPL_FC * 3136 * 512, s_c3 = (size_t)SPL_C3 * 576 * 64,
+                 s_c2 = (size_t)SPL_C2 * 512 * 64, s_c1 = (size_t)SPL_C1 * 256 * 32,
+                 s_h = (size_t)SPL_H * 512 * 32;
+    I->slab_floats = std::max(std::max(s_fc, s_c3), std::max(std::max(s_c2, s_c1), s_h)) + 1024 * 512;
+    ok = ok && dmalloc(I, &I->slab, I->slab_floats);
+    if (!ok) {
+        set_error("atari: hipMalloc failed for activations");
+        atari_destroy(n);
+        return nullptr;
+    }
+    return n;
+}
+
+void atari_destroy(AtariNet* n) {
+    if (!n) return;
+    AtariImpl* I = impl(n);
+    if (I) {
+        for (void* p : I->allocs) (void)hipFree(p);
+        delete I;
+    }
+    delete n;
+}
+
+int atari_sync_weights(AtariNet* n, const float* params, hipStream_t s) {
+    // fp32 master params -> the bf16 operand layouts of every forward / dgrad GEMM
+    AtariImpl* I = impl(n);
+    I->params = params;
+    hipLaunchKernelGGL(weights_bf16_kernel, dim3(2048), dim3(256), 0, s, params, I->off, I->A, I->wb);
+    FI_HIP_CHECK(hipGetLastError());
+    return FI_OK;
+}
+
+int atari_forward(AtariNet* n, const uint8_t* frames, float* logits, float* values, hipStream_t s,
+                  KernelTagger* tg) {
+    AtariImpl* I = impl(n);
+    const int N = I->N;
+    const float* p = I->params;
+    const Offsets& o = I->off;
+    using namespace geo;
+    int rc;
+    { TagScope ts(tg, "conv1_fwd"); rc = gemm<256, 32, 4, 1>(Conv1Gather{frames, N * P1}, RowsBf16{I->wb.c1T, C1O, C1K},
+                             EpiAct{I->a1, C1O, p + o.c1b, 1.0f / 255.0f}, N * P1, C1O, C1K, s); }
+    if (rc) return rc;
+    { TagScope ts(tg, "conv2_fwd"); rc = gemm<128, 64, 2, 2>(ConvGather<20, 32, 4, 2, 9>{I->a1, N * P2}, RowsBf16{I->wb.c2T, C2O, C2K},
+                             EpiAct{I->a2, C2O, p + o.c2b, 1.0f}, N * P2, C2O, C2K, s); }
+    if (rc) return rc;
+    { TagScope ts(tg, "conv3_fwd"); rc = gemm<128, 64, 2, 2>(ConvGather<9, 64, 3, 1, 7>{I->a2, N * P3}, RowsBf16{I->wb.c3T, C3O, C3K},
+                             EpiAct{I->a3, C3O, p + o.c3b, 1.0f}, N * P3, C3O, C3K, s); }
+    if (rc) return rc;
+    { TagScope ts(tg, "fc_fwd"); rc = gemm<128, 128, 2, 2>(RowsBf16{I->a3, N, FCK}, RowsBf16{I->wb.fcT, FCO, FCK},
+                              EpiAct{I->h, FCO, p + o.fcb, 1.0f}, N, FCO, FCK, s); }
+    if (rc) return rc;
+    { TagScope ts(tg, "heads_fwd"); rc = gemm<128, 32, 4, 1>(RowsBf16{I->h, N, FCO}, RowsBf16{I->wb.hT, HP, FCO},
+                             EpiHeadsOut{logits, values, p + o.hb, I->A}, N, HP, FCO, s); }
+    return rc;
+}
+
+int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, const float* dvalue,
+                   float* grads, hipStream_t s, KernelTagger* tg) {
+    AtariImpl* I = impl(n);
+    const int N = I->N, A = I->A, O = A + 1;
+    const Offsets& o = I->off;
+    using namespace geo;
+    float* slab = I->slab;
+    float* cs = I->slab + I->slab_floats - 1024 * 512;
+    DoutRows dout{dlogits, dvalue, N, I->TB, A};
+    int rc;
+#define FI_A(tag, x) do { TagScope ts_(tg, tag); rc = (x); if (rc) return rc; } while (0)
+    // heads: wgrad [512][O] + bias, dgrad -> dh (masked by h)
+    FI_A("heads_wgrad", (wgrad<128, 32, 4, 1>(RowsBf16{I->h, N, FCO}, dout, slab, cs, N, FCO, O, SPL_H, 1.f, s)));
+    FI_A("reduce_slabs", reduce_slabs(slab, SPL_H, (size_t)FCO * O, grads + o.hw, s));
+    FI_A("reduce_slabs", reduce_slabs(cs, SPL_H, (size_t)O, grads + o.hb, s));
+    FI_A("heads_dgrad", (gemm<128, 128, 2, 2>(dout, RowsBf16{I->wb.hD, FCO, HP}, EpiMaskBf16{I->dh, I->h, FCO}, N, FCO,
+                               HP, s)));
+    // fc: wgrad [3136][512] + bias, dgrad -> da3 (masked by a3)
+    FI_A("fc_wgrad", (wgrad<128, 128, 2, 2>(RowsBf16{I->a3, N, FCK}, RowsBf16{I->dh, N, FCO}, slab, cs, N, FCK, FCO,
+                                SPL_FC, 1.f, s)));
+    FI_A("reduce_slabs", reduce_slabs(slab, SPL_FC, (size_t)FCK * FCO, grads + o.fcw, s));
+    FI_A("reduce_slabs", reduce_slabs(cs, SPL_FC, (size_t)FCO, grads + o.fcb, s));
+    FI_A("fc_dgrad", (gemm<128, 128, 2, 2>(RowsBf16{I->dh, N, FCO}, RowsBf16{I->wb.fcB, FCK, FCO},
+                               EpiMaskBf16{I->da3, I->a3, FCK}, N, FCK, FCO, s)));
+    // conv3: wgrad [576][64] + bias, dgrad -> da2 (masked by a2)
+    FI_A("conv3_wgrad", (wgrad<128, 64, 2, 2>(ConvGather<9, 64, 3, 1, 7>{I->a2, N * P3}, RowsBf16{I->da3, N * P3, C3O},
+                               slab, cs, N * P3, C3K, C3O, SPL_C3, 1.f, s)));
+    FI_A("reduce_slabs", reduce_slabs(slab, SPL_C3, (size_t)C3K * C3O, grads + o.c3w, s));
+    FI_A("reduce_slabs", reduce_slabs(cs, SPL_C3, (size_t)C3O, grads + o.c3b, s));
+    FI_A("conv3_dgrad", (gemm<128, 64, 2, 2>(DgradGather<9, 3, 1, 7, 64>{I->da3, N, I->cs3},
+                              ClassRows{I->wb.c3D, 64, C3K, I->cs3, (size_t)64 * C3K, nullptr},
+                              EpiDgrad<9, 1>{I->da2, I->a2, N, I->cs3, 64}, I->cs3, 64, C3K, s)));
+    // conv2: wgrad [512][64] + bias, dgrad -> da1 (4 parity classes, masked by a1)
+    FI_A("conv2_wgrad", (wgrad<128, 64, 2, 2>(ConvGather<20, 32, 4, 2, 9>{I->a1, N * P2}, RowsBf16{I->da2, N * P2, C2O},
+                               slab, cs, N * P2, C2K, C2O, SPL_C2, 1.f, s)));
+    FI_A("reduce_slabs", reduce_slabs(slab, SPL_C2, (size_t)C2K * C2O, grads + o.c2w, s));
+    FI_A("reduce_slabs", reduce_slabs(cs, SPL_C2, (size_t)C2O, grads + o.c2b, s));
+    FI_A("conv2_dgrad", (gemm<128, 32, 4, 1>(DgradGather<20, 4, 2, 9, 64>{I->da2, N, I->cs2},
+                              ClassRows{I->wb.c2D, 32, 256, I->cs2, (size_t)32 * 256, nullptr},
+                              EpiDgrad<20, 2>{I->da1, I->a1, N, I->cs2, 32}, 4 * I->cs2, 32, 256, s)));
+    // conv1: wgrad [256][32] (+1/255 input scale) + bias
+    FI_A("conv1_wgrad", (wgrad<128, 32, 4, 1>(Conv1Gather{frames, N * P1}, RowsBf16{I->da1, N * P1, C1O}, slab, cs,
+                               N * P1, C1K, C1O, SPL_C1, 1.0f / 255.0f, s)));
+    FI_A("reduce_slabs", reduce_slabs(slab, SPL_C1, (size_t)C1K * C1O, grads + o.c1w, s));
+    FI_A("reduce_slabs", reduce_slabs(cs, SPL_C1, (size_t)C1O, grads + o.c1b, s));
+#undef FI_A
+    return FI_OK;
+}
+
+bool atari_tensor(AtariNet* n, const char* name, void** p, size_t* bytes) {
+    AtariImpl* I = impl(n);
+    const size_t N = I->N;
+    struct E {
+        const char* nm;
+        void* p;
+        size_t b;
+    } t[] = {{"a1", I->a1, N * 400 * 32 * 2}, {"a2", I->a2, N * 81 * 64 * 2},
+             {"a3", I->a3, N * 3136 * 2},     {"h", I->h, N * 512 * 2},
+             {"da1", I->da1, N * 400 * 32 * 2}, {"da2", I->da2, N * 81 * 64 * 2},
+             {"da3", I->da3, N * 3136 * 2},   {"dh", I->dh, N * 512 * 2}};
+    for (auto& e : t)
+        if (std::string(e.nm) == name) {
+            *p = e.p;
+            *bytes = e.b;
+            return true;
+        }
+    return false;
+}
+
 }  // namespace fi

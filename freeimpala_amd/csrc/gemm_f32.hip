@@ -210,9 +210,11 @@ struct EpiSlab {  // split-K partial slab: C[split][m][n]
 };
 
 // ---------------- the kernel --------------------------------------------------------
-template <class LA, class LB, class Epi>
+// COLSUM: blocks of the first M-tile also sum the B tile over k (the bias gradient of a
+// weight-gradient GEMM, B = dY) into colsum[split][N] -- no separate column-sum pass.
+template <class LA, class LB, class Epi, bool COLSUM>
 __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(LA la, LB lb, Epi epi, int M, int N,
-                                                          int K, int k_per_split) {
+                                                          int K, int k_per_split, float* colsum) {
     __shared__ __attribute__((aligned(16))) float As[2][GBK * GLDA];
     __shared__ __attribute__((aligned(16))) float Bs[2][GBK * GLDB];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -220,6 +222,8 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(LA la, LB lb, Epi epi,
     const int kbeg = blockIdx.z * k_per_split;
     const int kend = min(K, kbeg + k_per_split);
     f32x16 acc0 = {}, acc1 = {};
+    float cs = 0.f;
+    const bool do_cs = COLSUM && blockIdx.x == 0 && threadIdx.x < GBN;
     typename RegsOf<LA>::type ra[RegsOf<LA>::N];
     typename RegsOf<LB>::type rb[RegsOf<LB>::N];
     int buf = 0;
@@ -247,6 +251,10 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(LA la, LB lb, Epi epi,
             acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b0, acc0, 0, 0, 0);
             acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b1, acc1, 0, 0, 0);
         }
+        if (do_cs) {
+#pragma unroll
+            for (int kk = 0; kk < GBK; ++kk) cs += bs[kk * GLDB + threadIdx.x];
+        }
         if (more) {
             la.store(As[buf ^ 1], GLDA, ra);
             lb.store(Bs[buf ^ 1], GLDB, rb);
@@ -254,6 +262,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(LA la, LB lb, Epi epi,
         __syncthreads();
         buf ^= 1;
     }
+    if (do_cs && n0 + (int)threadIdx.x < N) colsum[(size_t)blockIdx.z * N + n0 + threadIdx.x] = cs;
     // C/D map of 32x32 tiles: row = (r&3) + 8*(r>>2) + 4*(lane>>5), col = lane&31
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -269,11 +278,16 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(LA la, LB lb, Epi epi,
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 template <class LA, class LB, class Epi>
-static int launch(LA la, LB lb, Epi epi, int M, int N, int K, int splits, hipStream_t s) {
+static int launch(LA la, LB lb, Epi epi, int M, int N, int K, int splits, hipStream_t s,
+                  float* colsum = nullptr) {
     const int kps = ((K + splits - 1) / splits + GBK - 1) / GBK * GBK;
     dim3 grid((M + GBM - 1) / GBM, (N + GBN - 1) / GBN, splits);
-    hipLaunchKernelGGL((gemm_f32_kernel<LA, LB, Epi>), grid, dim3(256), 0, s, la, lb, epi, M, N, K,
-                       kps);
+    if (colsum)
+        hipLaunchKernelGGL((gemm_f32_kernel<LA, LB, Epi, true>), grid, dim3(256), 0, s, la, lb, epi, M,
+                           N, K, kps, colsum);
+    else
+        hipLaunchKernelGGL((gemm_f32_kernel<LA, LB, Epi, false>), grid, dim3(256), 0, s, la, lb, epi,
+                           M, N, K, kps, colsum);
     FI_HIP_CHECK(hipGetLastError());
     return FI_OK;
 }
@@ -314,19 +328,20 @@ int f32_heads_dgrad(const HeadsGrad& g, const float* W, int K, const float* act,
 }
 
 // partial weight gradients: slab[split][I][N] = sum_{m in split} X[m][I] dY[m][N]
+// slab[split][I][N] = sum_{m in split} X[m][I] dY[m][N];  cs_slab[split][N] = sum_m dY[m][N]
 int f32_linear_wgrad_partial(const float* X, int M, int I, const float* dY, int N, int splits,
-                             float* slab, hipStream_t s) {
+                             float* slab, float* cs_slab, hipStream_t s) {
     KMajor<GBM> la{X, I, M, I, I % 4 == 0 && aligned16(X)};
     KMajor<GBN> lb{dY, N, M, N, N % 4 == 0 && aligned16(dY)};
-    return launch(la, lb, EpiSlab{slab, N, (size_t)I * N}, I, N, M, splits, s);
+    return launch(la, lb, EpiSlab{slab, N, (size_t)I * N}, I, N, M, splits, s, cs_slab);
 }
 
 int f32_heads_wgrad_partial(const float* X, int I, const HeadsGrad& g, int splits, float* slab,
-                            hipStream_t s) {
+                            float* cs_slab, hipStream_t s) {
     const int N = g.A + 1;
     KMajor<GBM> la{X, I, g.rows, I, I % 4 == 0 && aligned16(X)};
     DoutKMajor<GBN> lb{g};
-    return launch(la, lb, EpiSlab{slab, N, (size_t)I * N}, I, N, g.rows, splits, s);
+    return launch(la, lb, EpiSlab{slab, N, (size_t)I * N}, I, N, g.rows, splits, s, cs_slab);
 }
 
 }  // namespace fi

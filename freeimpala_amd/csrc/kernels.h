@@ -36,9 +36,9 @@ int f32_linear_dgrad(const float* dY, int M, int N, const float* W, int K, const
 int f32_heads_dgrad(const HeadsGrad& g, const float* W, int K, const float* act, float* dX,
                     hipStream_t s);
 int f32_linear_wgrad_partial(const float* X, int M, int I, const float* dY, int N, int splits,
-                             float* slab, hipStream_t s);
+                             float* slab, float* cs_slab, hipStream_t s);
 int f32_heads_wgrad_partial(const float* X, int I, const HeadsGrad& g, int splits, float* slab,
-                            hipStream_t s);
+                            float* cs_slab, hipStream_t s);
 
 // misc.hip
 int colsum_partial(const float* Y, int M, int N, int splits, float* slab, hipStream_t s);

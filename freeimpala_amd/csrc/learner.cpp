@@ -181,7 +181,7 @@ static void destroy(fi_learner* l) {
     if (!l) return;
     if (l->stream) hipStreamSynchronize(l->stream);
     if (l->comm) ncclCommDestroy(l->comm);
-    delete l->atari;
+    atari_destroy(l->atari);
     for (void* p : l->allocs) hipFree(p);
     if (l->pinned) hipHostFree(l->pinned);
     for (auto& e : l->ev)
@@ -252,7 +252,7 @@ static int create(const fi_learner_config* cfg, fi_learner** out) {
         FI_TRY(dalloc_n(l, &l->dz2, rows * H));
         l->splits = (int)std::min<size_t>(128, std::max<size_t>(1, rows / 2048));
         const size_t big = std::max<size_t>((size_t)D * H, (size_t)H * H);
-        l->slab_floats = (size_t)l->splits * (big + H + 64);
+        l->slab_floats = (size_t)l->splits * (big + 4096);  // wgrad slabs | bias colsum slabs
         FI_TRY(dalloc_n(l, &l->slab, l->slab_floats));
     } else {
         l->atari = atari_create(l->B, l->T, A);
@@ -349,6 +349,21 @@ struct Tag {
     }
 };
 
+// the same events, driven from inside the Atari net's launch sequence
+struct LearnerTagger : KernelTagger {
+    fi_learner* l;
+    std::vector<Tag*> open;
+    explicit LearnerTagger(fi_learner* l_) : l(l_) {}
+    void begin(const char* name) override { open.push_back(new Tag(l, name)); }
+    void end() override {
+        delete open.back();
+        open.pop_back();
+    }
+    ~LearnerTagger() override {
+        for (Tag* t : open) delete t;
+    }
+};
+
 static void collect_tags(fi_learner* l) {
     for (int i = 0; i < l->tag_used; ++i) {
         float ms = 0.f;
@@ -382,10 +397,10 @@ static int mlp_forward(fi_learner* l) {
 
 static int wgrad(fi_learner* l, const char* tag, const float* X, int I, const float* dY, int N,
                  float* gW, float* gb) {
-    { Tag t(l, tag); FI_TRY(f32_linear_wgrad_partial(X, l->rows, I, dY, N, l->splits, l->slab, l->stream)); }
+    float* cs = l->slab + l->slab_floats - (size_t)l->splits * 4096;
+    { Tag t(l, tag); FI_TRY(f32_linear_wgrad_partial(X, l->rows, I, dY, N, l->splits, l->slab, cs, l->stream)); }
     { Tag t(l, "reduce_slabs"); FI_TRY(reduce_slabs(l->slab, l->splits, (size_t)I * N, gW, l->stream)); }
-    { Tag t(l, "colsum"); FI_TRY(colsum_partial(dY, l->rows, N, l->splits, l->slab, l->stream)); }
-    { Tag t(l, "reduce_slabs"); FI_TRY(reduce_slabs(l->slab, l->splits, (size_t)N, gb, l->stream)); }
+    { Tag t(l, "reduce_slabs"); FI_TRY(reduce_slabs(cs, l->splits, (size_t)N, gb, l->stream)); }
     return FI_OK;
 }
 
@@ -400,10 +415,10 @@ static int mlp_backward(fi_learner* l) {
     float* gWh = gb2 + H;
     float* gbh = gWh + (size_t)H * O;
     HeadsGrad g{l->dlogits, l->dvalue, l->rows, l->TB, A};
-    { Tag t(l, "mlp_wgrad_heads"); FI_TRY(f32_heads_wgrad_partial(l->h2, H, g, l->splits, l->slab, l->stream)); }
+    float* cs = l->slab + l->slab_floats - (size_t)l->splits * 4096;
+    { Tag t(l, "mlp_wgrad_heads"); FI_TRY(f32_heads_wgrad_partial(l->h2, H, g, l->splits, l->slab, cs, l->stream)); }
     { Tag t(l, "reduce_slabs"); FI_TRY(reduce_slabs(l->slab, l->splits, (size_t)H * O, gWh, l->stream)); }
-    { Tag t(l, "colsum"); FI_TRY(heads_colsum_partial(g, l->splits, l->slab, l->stream)); }
-    { Tag t(l, "reduce_slabs"); FI_TRY(reduce_slabs(l->slab, l->splits, (size_t)O, gbh, l->stream)); }
+    { Tag t(l, "reduce_slabs"); FI_TRY(reduce_slabs(cs, l->splits, (size_t)O, gbh, l->stream)); }
     { Tag t(l, "mlp_dgrad_heads"); FI_TRY(f32_heads_dgrad(g, Wh, H, l->h2, l->dz2, l->stream)); }
     FI_TRY(wgrad(l, "mlp_wgrad_l2", l->h1, H, l->dz2, H, gW2, gb2));
     { Tag t(l, "mlp_dgrad_l2"); FI_TRY(f32_linear_dgrad(l->dz2, l->rows, H, W2, H, l->h1, l->dz1, l->stream)); }
@@ -424,7 +439,10 @@ static int run_step(fi_learner* l, bool have_host_batch, fi_step_stats* out) {
     }
     mark(l, FI_PHASE_FORWARD);
     if (l->cfg.arch == FI_ARCH_MLP) FI_TRY(mlp_forward(l));
-    else FI_TRY(atari_forward(l->atari, l->frames, l->logits, l->values, l->stream));
+    else {
+        LearnerTagger tg(l);
+        FI_TRY(atari_forward(l->atari, l->frames, l->logits, l->values, l->stream, l->profiling ? &tg : nullptr));
+    }
     mark(l, FI_PHASE_VTRACE);
     {
         int nblk = 0;
@@ -439,8 +457,11 @@ static int run_step(fi_learner* l, bool have_host_batch, fi_step_stats* out) {
     }
     mark(l, FI_PHASE_BACKWARD);
     if (l->cfg.arch == FI_ARCH_MLP) FI_TRY(mlp_backward(l));
-    else
-        FI_TRY(atari_backward(l->atari, l->frames, l->dlogits, l->dvalue, l->grads, l->stream));
+    else {
+        LearnerTagger tg(l);
+        FI_TRY(atari_backward(l->atari, l->frames, l->dlogits, l->dvalue, l->grads, l->stream,
+                              l->profiling ? &tg : nullptr));
+    }
     mark(l, FI_PHASE_ALLREDUCE);
     if (l->comm) {
         Tag t(l, "allreduce");

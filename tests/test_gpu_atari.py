@@ -1,0 +1,100 @@
+"""GPU parity of the Atari-shaped conv policy (config #3 network) against the oracle.
+
+The product computes the GEMMs on bf16 MFMA with fp32 accumulation and keeps activations /
+upstream gradients in bf16; the oracle runs in its bf16-emulation mode (every GEMM operand
+rounded to bf16, fp64 accumulation). Remaining differences are fp32-vs-fp64 accumulation and
+the rare bf16 rounding flip they cause, so tensors are compared by relative L2 norm
+(<= 2e-3) and scaled max error (<= 2e-2). V-trace outputs keep the 1e-5 fp32 bar.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def bf16_to_f32(u16):
+    return (np.asarray(u16, np.uint16).astype(np.uint32) << 16).view(np.float32)
+
+
+def rel(a, b, what, l2=2e-3, mx=2e-2):
+    a = np.asarray(a, np.float64).ravel()
+    b = np.asarray(b, np.float64).ravel()
+    assert np.isfinite(a).all(), what
+    e2 = np.linalg.norm(a - b) / max(1e-30, np.linalg.norm(b))
+    em = np.abs(a - b).max() / max(1e-30, np.abs(b).max())
+    assert e2 <= l2 and em <= mx, f"{what}: rel L2 {e2:.2e} scaled max {em:.2e}"
+
+
+def mk(T=2, B=16, A=18, **kw):
+    from freeimpala_amd.learner import DeviceLearner
+    kw.setdefault("optimizer", "sgd")
+    kw.setdefault("lr", 1e-3)
+    kw.setdefault("max_grad_norm", 0.0)
+    return DeviceLearner("atari", seq_len=T, batch=B, num_actions=A, **kw)
+
+
+def test_atari_synth_frames_bit_exact(orc):
+    L = mk(T=1, B=16)
+    L.synth(seed=9, b_global=32, b_offset=16)
+    ref = orc.synth_batch(9, T=1, B=16, A=18, D=1, B_glob=32, b_off=16, obs=False, frames=True)
+    np.testing.assert_array_equal(L.tensor("frames", np.uint8, (2, 16, 84, 84, 4)), ref["frames"])
+    np.testing.assert_array_equal(L.tensor("actions", np.int32, (1, 16)), ref["actions"])
+
+
+@pytest.mark.parametrize("T,B", [(2, 16), (3, 32)])
+def test_atari_forward_backward_parity(orc, T, B):
+    A = 18
+    L = mk(T=T, B=B, A=A)
+    L.synth(seed=T * 100 + B)
+    N = (T + 1) * B
+    frames = L.tensor("frames", np.uint8, (N, 84, 84, 4))
+    p0 = L.get_params()
+    st = L.step_resident()
+    acts = orc.atari_forward(frames, p0, A=A, bf16_emul=True)
+    for name, shape in [("a1", (N, 20, 20, 32)), ("a2", (N, 9, 9, 64)), ("a3", (N, 7, 7, 64)),
+                        ("h", (N, 512))]:
+        gpu = bf16_to_f32(L.tensor(name, np.uint16, shape))
+        rel(gpu, orc.bf16_round(acts[name]), name)
+    logits = L.tensor("logits", shape=(T + 1, B, A))
+    values = L.tensor("values", shape=(T + 1, B))
+    rel(logits.reshape(N, A), acts["out"][:, :A], "logits")
+    rel(values.reshape(N), acts["out"][:, A], "values")
+    # V-trace on the GPU's own logits must match the oracle at the 1e-5 fp32 bar
+    batch = dict(mu=L.tensor("mu", shape=(T, B, A)), actions=L.tensor("actions", np.int32, (T, B)),
+                 rewards=L.tensor("rewards", shape=(T, B)), discounts=L.tensor("discounts", shape=(T, B)))
+    vt = orc.vtrace_loss(logits[:T], batch["mu"], batch["actions"], batch["rewards"],
+                         batch["discounts"], values)
+    dl = L.tensor("dlogits", shape=(T, B, A))
+    dv = L.tensor("dvalue", shape=(T + 1, B))
+    assert np.abs(dl - vt["dlogits"]).max() <= 1e-5 * max(1, np.abs(vt["dlogits"]).max())
+    assert np.abs(dv - vt["dvalue"]).max() <= 1e-5 * max(1, np.abs(vt["dvalue"]).max())
+    tot = orc.total_loss(vt["losses"])
+    assert abs(st["total_loss"] - tot) <= 1e-5 * max(1.0, abs(tot))
+    # backward with the same upstream gradient
+    dout = np.zeros((N, A + 1), np.float32)
+    dout[:T * B, :A] = dl.reshape(T * B, A)
+    dout[:, A] = dv.reshape(N)
+    g_ref = orc.atari_backward(frames, p0, acts, dout, A=A, bf16_emul=True)
+    g = L.tensor("grads")
+    sizes = [8192, 32, 32768, 64, 36864, 64, 3136 * 512, 512, 512 * (A + 1), A + 1]
+    names = ["c1W", "c1b", "c2W", "c2b", "c3W", "c3b", "fcW", "fcb", "hW", "hb"]
+    off = np.cumsum([0] + sizes)
+    for i, nm in enumerate(names):
+        rel(g[off[i]:off[i + 1]], g_ref[off[i]:off[i + 1]], nm, l2=5e-3, mx=5e-2)
+    # SGD update uses exactly the gradient the kernels produced
+    np.testing.assert_allclose(L.get_params(), p0 - np.float32(1e-3) * g, rtol=0, atol=1e-6)
+
+
+def test_atari_training_reduces_loss():
+    L = mk(T=4, B=32, optimizer="adam", lr=3e-4, max_grad_norm=40.0)
+    L.synth(seed=1)
+    losses = [L.step_resident()["total_loss"] for _ in range(20)]
+    assert np.isfinite(losses).all()
+    assert losses[-1] < losses[0]
+
+
+def test_atari_publish_fits_actor_buffer():
+    """Published bf16 weights must fit the MPI actors' fixed 6 MiB receive buffer
+    (reference cmd/freeimpala_mpi_*/main.cpp model size, agent.h:131-138)."""
+    L = mk(T=1, B=16, publish="bf16")
+    assert L.param_bytes == 2 * 1693875 <= 6 * 1024 * 1024

@@ -18,6 +18,18 @@ def scaled_close(a, b, tol=1e-5, what=""):
     assert err <= tol, f"{what}: scaled err {err:.3e}"
 
 
+def grads_close(a, b, what="", rel_l2=1e-5, rel_max=3e-4):
+    """fp32 GEMM gradients vs the fp64 oracle: reductions over (T+1)*B rows accumulate in fp32
+    (MFMA), so elementwise error scales with sum|terms|, not |result|. Criterion per tensor:
+    ||d||_2 <= rel_l2 ||ref||_2 and max|d| <= rel_max * max|ref|."""
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    assert np.isfinite(a).all(), what
+    l2 = np.linalg.norm(a - b) / max(1e-30, np.linalg.norm(b))
+    mx = np.abs(a - b).max() / max(1e-30, np.abs(b).max())
+    assert l2 <= rel_l2 and mx <= rel_max, f"{what}: rel L2 {l2:.2e}, rel max {mx:.2e}"
+
+
 def mk(T=5, B=16, A=18, D=128, H=256, **kw):
     from freeimpala_amd.learner import DeviceLearner
     kw.setdefault("optimizer", "sgd")
@@ -68,7 +80,7 @@ def test_mlp_step_parity(orc, T, B):
     D, H, A = 128, 256, 18
     off = np.cumsum([0, D * H, H, H * H, H, H * (A + 1), A + 1])
     for i, name in enumerate(["W1", "b1", "W2", "b2", "Wh", "bh"]):
-        scaled_close(g[off[i]:off[i + 1]], ref["grads"][off[i]:off[i + 1]], what=name)
+        grads_close(g[off[i]:off[i + 1]], ref["grads"][off[i]:off[i + 1]], what=name)
     tot = ref["vt"]["losses"]
     assert abs(st["pg_loss"] - tot[0]) <= 1e-5 * max(1, abs(tot[0]))
     assert abs(st["baseline_loss"] - tot[1]) <= 1e-5 * max(1, abs(tot[1]))
@@ -93,7 +105,11 @@ def test_mlp_config2_full_size(orc):
     scaled_close(L.tensor("pg_adv", shape=(T, B)), ref["vt"]["pg_adv"], what="pg_adv")
     scaled_close(L.tensor("dlogits", shape=(T, B, 18)), ref["vt"]["dlogits"], what="dlogits")
     scaled_close(L.tensor("dvalue", shape=(T + 1, B)), ref["vt"]["dvalue"], what="dvalue")
-    scaled_close(L.tensor("grads"), ref["grads"], 2e-5, what="grads")
+    g = L.tensor("grads")
+    D, H, A = 128, 256, 18
+    off = np.cumsum([0, D * H, H, H * H, H, H * (A + 1), A + 1])
+    for i, name in enumerate(["W1", "b1", "W2", "b2", "Wh", "bh"]):
+        grads_close(g[off[i]:off[i + 1]], ref["grads"][off[i]:off[i + 1]], what=name)
 
 
 def test_adam_and_clip_match_oracle(orc):
