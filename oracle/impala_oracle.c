@@ -414,9 +414,24 @@ int orc_atari_forward(int N, int A, const uint8_t* frames, const float* params, 
     return 0;
 }
 
+/* as orc_atari_backward, optionally returning the intermediate (masked) data gradients
+ * dh (N,512), d3 (N,3136), d2 (N,81*64), d1 (N,400*32) -- any may be NULL */
+int orc_atari_backward_ex(int N, int A, const uint8_t* frames, const float* params, int emul,
+                          const float* a1, const float* a2, const float* a3, const float* h,
+                          const float* dout, float* grads, float* dh_out, float* d3_out,
+                          float* d2_out, float* d1_out);
+
 int orc_atari_backward(int N, int A, const uint8_t* frames, const float* params, int emul,
                        const float* a1, const float* a2, const float* a3, const float* h,
                        const float* dout, float* grads) {
+    return orc_atari_backward_ex(N, A, frames, params, emul, a1, a2, a3, h, dout, grads, NULL,
+                                 NULL, NULL, NULL);
+}
+
+int orc_atari_backward_ex(int N, int A, const uint8_t* frames, const float* params, int emul,
+                          const float* a1, const float* a2, const float* a3, const float* h,
+                          const float* dout, float* grads, float* dh_out, float* d3_out,
+                          float* d2_out, float* d1_out) {
     size_t off[10]; atari_offsets(A, off);
     int O = A + 1;
     size_t nx = (size_t)N * AT_H * AT_H * AT_C;
@@ -436,6 +451,10 @@ int orc_atari_backward(int N, int A, const uint8_t* frames, const float* params,
     conv_wgrad(N, 20, 32, 4, 2, 64, a1, d2, 1.0f, emul, grads + off[2], grads + off[3]);
     conv_dgrad(N, 20, 32, 4, 2, 64, d2, params + off[2], a1, emul, d1);
     conv_wgrad(N, 84, 4, 8, 4, 32, x0, d1, 1.0f / 255.0f, emul, grads + off[0], grads + off[1]);
+    if (dh_out) memcpy(dh_out, dh, (size_t)N * 512 * sizeof(float));
+    if (d3_out) memcpy(d3_out, d3, (size_t)N * 3136 * sizeof(float));
+    if (d2_out) memcpy(d2_out, d2, (size_t)N * 81 * 64 * sizeof(float));
+    if (d1_out) memcpy(d1_out, d1, (size_t)N * 400 * 32 * sizeof(float));
     free(x0); free(dh); free(d3); free(d2); free(d1);
     return 0;
 }

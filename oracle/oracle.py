@@ -56,6 +56,7 @@ def lib():
         L.orc_atari_param_count.restype = C.c_size_t
         L.orc_atari_forward.argtypes = [C.c_int, C.c_int, P, P, C.c_int, P, P, P, P, P]
         L.orc_atari_backward.argtypes = [C.c_int, C.c_int, P, P, C.c_int, P, P, P, P, P, P]
+        L.orc_atari_backward_ex.argtypes = [C.c_int, C.c_int, P, P, C.c_int] + [P] * 10
         L.orc_clip_grad_norm.argtypes = [C.c_size_t, P, C.c_double]
         L.orc_clip_grad_norm.restype = C.c_double
         L.orc_adam.argtypes = [C.c_size_t, P, P, P, P, C.c_float, C.c_float, C.c_float,
@@ -161,6 +162,21 @@ def atari_backward(frames, params, acts, dout, A=18, bf16_emul=True):
                                   _p(acts["h"]), _p(_f32(dout)), _p(g))
     assert rc == 0
     return g
+
+
+def atari_backward_ex(frames, params, acts, dout, A=18, bf16_emul=True):
+    """Returns (grads, dict(dh, d3, d2, d1)) -- the masked data gradients of every layer."""
+    frames = np.ascontiguousarray(frames, dtype=np.uint8)
+    N = frames.shape[0]
+    g = np.empty(atari_param_count(A), np.float32)
+    mids = dict(dh=np.empty((N, 512), np.float32), d3=np.empty((N, 7, 7, 64), np.float32),
+                d2=np.empty((N, 9, 9, 64), np.float32), d1=np.empty((N, 20, 20, 32), np.float32))
+    rc = lib().orc_atari_backward_ex(N, A, _p(frames), _p(_f32(params)), int(bf16_emul),
+                                     _p(acts["a1"]), _p(acts["a2"]), _p(acts["a3"]), _p(acts["h"]),
+                                     _p(_f32(dout)), _p(g), _p(mids["dh"]), _p(mids["d3"]),
+                                     _p(mids["d2"]), _p(mids["d1"]))
+    assert rc == 0
+    return g, mids
 
 
 def clip_grad_norm(g, max_norm):

@@ -70,27 +70,36 @@ def test_atari_forward_backward_parity(orc, T, B):
     assert np.abs(dv - vt["dvalue"]).max() <= 1e-5 * max(1, np.abs(vt["dvalue"]).max())
     tot = orc.total_loss(vt["losses"])
     assert abs(st["total_loss"] - tot) <= 1e-5 * max(1.0, abs(tot))
-    # backward with the same upstream gradient
+    # backward: the oracle gets the GPU's own activations and upstream gradient (identical
+    # ReLU masks -- a pre-activation within rounding of 0 may flip sign between fp32 and fp64
+    # accumulation, which is a forward difference, not a backward one)
     dout = np.zeros((N, A + 1), np.float32)
     dout[:T * B, :A] = dl.reshape(T * B, A)
     dout[:, A] = dv.reshape(N)
-    g_ref = orc.atari_backward(frames, p0, acts, dout, A=A, bf16_emul=True)
+    gpu_acts = {nm: bf16_to_f32(L.tensor(nm, np.uint16, sh)) for nm, sh in
+                [("a1", (N, 20, 20, 32)), ("a2", (N, 9, 9, 64)), ("a3", (N, 7, 7, 64)), ("h", (N, 512))]}
+    g_ref, mids = orc.atari_backward_ex(frames, p0, gpu_acts, dout, A=A, bf16_emul=True)
+    for nm, key, sh in [("dh", "dh", (N, 512)), ("da3", "d3", (N, 7, 7, 64)),
+                        ("da2", "d2", (N, 9, 9, 64)), ("da1", "d1", (N, 20, 20, 32))]:
+        rel(bf16_to_f32(L.tensor(nm, np.uint16, sh)), orc.bf16_round(mids[key]), nm)
     g = L.tensor("grads")
     sizes = [8192, 32, 32768, 64, 36864, 64, 3136 * 512, 512, 512 * (A + 1), A + 1]
     names = ["c1W", "c1b", "c2W", "c2b", "c3W", "c3b", "fcW", "fcb", "hW", "hb"]
     off = np.cumsum([0] + sizes)
     for i, nm in enumerate(names):
-        rel(g[off[i]:off[i + 1]], g_ref[off[i]:off[i + 1]], nm, l2=5e-3, mx=5e-2)
+        rel(g[off[i]:off[i + 1]], g_ref[off[i]:off[i + 1]], nm)
     # SGD update uses exactly the gradient the kernels produced
     np.testing.assert_allclose(L.get_params(), p0 - np.float32(1e-3) * g, rtol=0, atol=1e-6)
 
 
 def test_atari_training_reduces_loss():
-    L = mk(T=4, B=32, optimizer="adam", lr=3e-4, max_grad_norm=40.0)
+    """gamma = 0 makes the V-trace target the (clipped) immediate reward, so the value loss of a
+    fixed batch is a plain regression that SGD must reduce."""
+    L = mk(T=4, B=32, optimizer="sgd", lr=2e-4, max_grad_norm=40.0, gamma=0.0)
     L.synth(seed=1)
-    losses = [L.step_resident()["total_loss"] for _ in range(20)]
-    assert np.isfinite(losses).all()
-    assert losses[-1] < losses[0]
+    base = [L.step_resident()["baseline_loss"] for _ in range(20)]
+    assert np.isfinite(base).all()
+    assert base[-1] < 0.9 * base[0]
 
 
 def test_atari_publish_fits_actor_buffer():
