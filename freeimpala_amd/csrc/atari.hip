@@ -18,6 +18,8 @@
 //    output pixels, so tiles are staged [m][i] and fed to the MFMA with the gfx950 transpose
 //    read ds_read_b64_tr_b16 (no shuffles); split over m into fp32 slabs reduced in a fixed
 //    order (deterministic); the bias gradient (column sums of B) rides along.
+#include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "atari.h"
@@ -521,7 +523,14 @@ struct AtariImpl {
     const float* params = nullptr;  // last synced fp32 params (for biases)
     std::vector<void*> allocs;
     int cs2 = 0, cs3 = 0;  // class strides for the dgrad GEMMs
+    bool fr = true;        // frame-resident kernels (FI_ATARI_GENERIC=1 -> generic GEMMs)
 };
+
+int conv1_fwd_fr_launch(const uint8_t* frames, const __bf16* w1t, const float* bias, __bf16* a1,
+                        int nframes, int grid, hipStream_t s);
+int conv1_wgrad_fr_launch(const uint8_t* frames, const __bf16* da1, float* slab, float* cs_slab,
+                          int nframes, int grid, hipStream_t s);
+constexpr int FR_GRID = 256;  // persistent frame-resident workgroups (1 per CU)
 
 static AtariImpl* impl(AtariNet* n) { return (AtariImpl*)n->impl; }
 
@@ -550,6 +559,7 @@ AtariNet* atari_create(int B, int T, int A) {
     n->B = B; n->T = T; n->A = A; n->N = (T + 1) * B;
     I->N = n->N; I->A = A; I->TB = T * B; I->off = Offsets(A);
     const size_t N = n->N;
+    I->fr = std::getenv("FI_ATARI_GENERIC") == nullptr;
     I->cs2 = (int)(((N * 100) + GBM - 1) / GBM * GBM);
     I->cs3 = (int)(((N * 81) + GBM - 1) / GBM * GBM);
     bool ok = dmalloc(I, &I->a1, N * 400 * 32) && dmalloc(I, &I->a2, N * 81 * 64) &&
@@ -601,7 +611,10 @@ int atari_forward(AtariNet* n, const uint8_t* frames, float* logits, float* valu
     const Offsets& o = I->off;
     using namespace geo;
     int rc;
-    { TagScope ts(tg, "conv1_fwd"); rc = gemm<256, 32, 4, 1>(Conv1Gather{frames, N * P1}, RowsBf16{I->wb.c1T, C1O, C1K},
+    if (I->fr) {
+        TagScope ts(tg, "conv1_fwd");
+        rc = conv1_fwd_fr_launch(frames, I->wb.c1T, p + o.c1b, I->a1, N, std::min(N, FR_GRID), s);
+    } else { TagScope ts(tg, "conv1_fwd"); rc = gemm<256, 32, 4, 1>(Conv1Gather{frames, N * P1}, RowsBf16{I->wb.c1T, C1O, C1K},
                              EpiAct{I->a1, C1O, p + o.c1b, 1.0f / 255.0f}, N * P1, C1O, C1K, s); }
     if (rc) return rc;
     { TagScope ts(tg, "conv2_fwd"); rc = gemm<128, 64, 2, 2>(ConvGather<20, 32, 4, 2, 9>{I->a1, N * P2}, RowsBf16{I->wb.c2T, C2O, C2K},
@@ -659,10 +672,17 @@ int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, con
                               ClassRows{I->wb.c2D, 32, 256, I->cs2, (size_t)32 * 256, nullptr},
                               EpiDgrad<20, 2>{I->da1, I->a1, N, I->cs2, 32}, 4 * I->cs2, 32, 256, s)));
     // conv1: wgrad [256][32] (+1/255 input scale) + bias
-    FI_A("conv1_wgrad", (wgrad<128, 32, 4, 1>(Conv1Gather{frames, N * P1}, RowsBf16{I->da1, N * P1, C1O}, slab, cs,
-                               N * P1, C1K, C1O, SPL_C1, 1.0f / 255.0f, s)));
-    FI_A("reduce_slabs", reduce_slabs(slab, SPL_C1, (size_t)C1K * C1O, grads + o.c1w, s));
-    FI_A("reduce_slabs", reduce_slabs(cs, SPL_C1, (size_t)C1O, grads + o.c1b, s));
+    if (I->fr) {
+        const int grid = std::min(N, FR_GRID);
+        FI_A("conv1_wgrad", conv1_wgrad_fr_launch(frames, I->da1, slab, cs, N, grid, s));
+        FI_A("reduce_slabs", reduce_slabs(slab, grid, (size_t)C1K * C1O, grads + o.c1w, s));
+        FI_A("reduce_slabs", reduce_slabs(cs, grid, (size_t)C1O, grads + o.c1b, s));
+    } else {
+        FI_A("conv1_wgrad", (wgrad<128, 32, 4, 1>(Conv1Gather{frames, N * P1}, RowsBf16{I->da1, N * P1, C1O}, slab, cs,
+                                   N * P1, C1K, C1O, SPL_C1, 1.0f / 255.0f, s)));
+        FI_A("reduce_slabs", reduce_slabs(slab, SPL_C1, (size_t)C1K * C1O, grads + o.c1w, s));
+        FI_A("reduce_slabs", reduce_slabs(cs, SPL_C1, (size_t)C1O, grads + o.c1b, s));
+    }
 #undef FI_A
     return FI_OK;
 }

@@ -1,0 +1,247 @@
+// atari_fr.hip -- frame-resident conv kernels for the Atari policy (gfx950).
+//
+// The generic implicit GEMM (atari.hip) re-gathers conv inputs per K-tile and waits on
+// memory latency every 32-deep K step. Every per-frame conv problem here is small enough
+// to keep the WHOLE frame on chip instead: a persistent workgroup stages one frame into
+// LDS with fully coalesced 16-byte loads (the next frame's loads are issued before the
+// current frame is computed, so HBM latency hides behind a frame of MFMAs), all MFMA
+// operands are then read from LDS, and outputs leave through an LDS staging tile as
+// coalesced 16-byte stores. HBM traffic is one read of each input byte and one write of
+// each output byte.
+//
+// conv1 (8x8/4, 4 -> 32 channels, u8 frames):
+//   LDS frame image: bf16, two "pair planes". A pair = 2 adjacent pixels x 4 channels =
+//   16 bytes; pair index q = x/2 goes to plane q&1 at slot y*21 + q/2. A 16-byte global
+//   load u of the frame (4 pixels) lands exactly in slot u of both planes. A forward A
+//   fragment (8 k = 2 pixels x 4 channels of one tap pair) of output pixel (oy, ox) is
+//   plane h, slot (4oy+ky)*21 + ox + (ks&1): consecutive output pixels hit consecutive
+//   16-byte slots (including across output-row wraps: 4*21 - 19 = 65 = 1 mod 16), so
+//   ds_read_b128 is bank-conflict free.
+#include "atari.h"
+#include "fi_common.h"
+#include "kernels.h"
+
+namespace fi {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+namespace c1 {
+constexpr int FRAME_LOADS = 84 * 84 * 4 / 16;       // 1764 16-byte loads per frame
+constexpr int PER_T = (FRAME_LOADS + 255) / 256;    // 7
+constexpr int PLANE = 84 * 21 * 16 + 64;            // bytes (+64: plane 1 shifted 4 slots)
+constexpr int IMG = 2 * PLANE;                      // 56,576 B
+constexpr int OUT = 400 * 32 * 2;                   // 25,600 B output / dY tile
+constexpr int OUT_CH = OUT / 16;                    // 1600 16-byte chunks
+constexpr int OUT_PER_T = (OUT_CH + 255) / 256;     // 7
+}  // namespace c1
+
+__device__ __forceinline__ void u8x16_to_bf16(u32x4 v, bf16x8& lo, bf16x8& hi) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        lo[j] = (__bf16)(float)((v[j >> 2] >> (8 * (j & 3))) & 0xffu);
+        hi[j] = (__bf16)(float)((v[2 + (j >> 2)] >> (8 * (j & 3))) & 0xffu);
+    }
+}
+
+__device__ __forceinline__ void c1_fetch_frame(const uint8_t* fr, u32x4 (&r)[c1::PER_T]) {
+    const u32x4* src = (const u32x4*)fr;
+#pragma unroll
+    for (int i = 0; i < c1::PER_T; ++i) {
+        const int u = threadIdx.x + 256 * i;
+        r[i] = u < c1::FRAME_LOADS ? __builtin_nontemporal_load(src + u) : u32x4{0, 0, 0, 0};
+    }
+}
+
+__device__ __forceinline__ void c1_store_image(char* img, const u32x4 (&r)[c1::PER_T]) {
+#pragma unroll
+    for (int i = 0; i < c1::PER_T; ++i) {
+        const int u = threadIdx.x + 256 * i;
+        if (u < c1::FRAME_LOADS) {
+            bf16x8 lo, hi;
+            u8x16_to_bf16(r[i], lo, hi);
+            *(bf16x8*)(img + 16 * u) = lo;
+            *(bf16x8*)(img + c1::PLANE + 16 * u) = hi;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// conv1 forward: a1[f] = bf16(relu(conv(frames[f]) / 255 + b)), persistent over frames
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 1) void conv1_fwd_fr(const uint8_t* __restrict__ frames,
+                                                       const __bf16* __restrict__ w1t,  // [32][256]
+                                                       const float* __restrict__ bias,
+                                                       __bf16* __restrict__ a1, int nframes) {
+    __shared__ __attribute__((aligned(16))) char smem[c1::IMG + c1::OUT];
+    char* img = smem;
+    __bf16* out = (__bf16*)(smem + c1::IMG);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, col = lane & 31;
+    // B fragments of all 16 K-steps stay in registers: lane holds W[n=col][k=16ks+8h..+8]
+    bf16x8 bw[16];
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) bw[ks] = *(const bf16x8*)(w1t + col * 256 + ks * 16 + h * 8);
+    const float bcol = bias[col];
+    const float inv255 = 1.0f / 255.0f;
+
+    u32x4 pre[c1::PER_T];
+    int f = blockIdx.x;
+    if (f < nframes) c1_fetch_frame(frames + (size_t)f * 28224, pre);
+    for (; f < nframes; f += gridDim.x) {
+        c1_store_image(img, pre);
+        const int fn = f + gridDim.x;
+        if (fn < nframes) c1_fetch_frame(frames + (size_t)fn * 28224, pre);
+        __syncthreads();  // image ready, previous out tile drained
+        // 13 row tiles of 32 output pixels: wave w takes tiles w, w+4, ...
+        for (int t = w; t < 13; t += 4) {
+            const int m = min(t * 32 + col, 399);
+            const int oy = m / 20, ox = m - oy * 20;
+            const char* abase = img + h * c1::PLANE + 16 * (oy * 4 * 21 + ox);
+            f32x16 acc = {};
+#pragma unroll
+            for (int ks = 0; ks < 16; ++ks) {
+                const bf16x8 a = *(const bf16x8*)(abase + 16 * ((ks >> 1) * 21 + (ks & 1)));
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bw[ks], acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (row < 400) out[row * 32 + col] = (__bf16)fmaxf(acc[r] * inv255 + bcol, 0.f);
+            }
+        }
+        __syncthreads();  // out tile complete, image free
+        u32x4* dst = (u32x4*)(a1 + (size_t)f * 12800);
+#pragma unroll
+        for (int i = 0; i < c1::OUT_PER_T; ++i) {
+            const int c = threadIdx.x + 256 * i;
+            if (c < c1::OUT_CH) __builtin_nontemporal_store(((const u32x4*)out)[c], dst + c);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// conv1 weight gradient: dW1[k][co] = 1/255 sum_{f,m} im2col(frame_f)[m][k] da1_f[m][co]
+// A^T fragments come from the frame image through ds_read_b64_tr_b16 with per-lane
+// gather addresses (each lane names one output pixel's 4 channels of one tap); da1 is
+// staged as [m][co] and read the same way. Each workgroup accumulates over its frames in
+// registers and writes one fp32 partial slab [256][32] + bias partial [32].
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ bf16x8 tr2(const char* p0, const char* p1) {
+    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)p0);
+    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)p1);
+    return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+__global__ __launch_bounds__(256, 1) void conv1_wgrad_fr(const uint8_t* __restrict__ frames,
+                                                         const __bf16* __restrict__ da1,
+                                                         float* __restrict__ slab,
+                                                         float* __restrict__ cs_slab, int nframes) {
+    __shared__ __attribute__((aligned(16))) char smem[c1::IMG + c1::OUT];
+    char* img = smem;
+    char* dy = smem + c1::IMG;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    // per-lane tr-read column: k = k0 + 16*(g&1) + 4p, i.e. tap = k0/4 + 4*(g&1) + p
+    f32x16 acc0 = {}, acc1 = {};
+    float csum[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // bias grad partial: co = 8*(chunk%4) + j
+
+    u32x4 pre[c1::PER_T], pdy[c1::OUT_PER_T];
+    auto fetch = [&](int ff) {
+        c1_fetch_frame(frames + (size_t)ff * 28224, pre);
+        const u32x4* s = (const u32x4*)(da1 + (size_t)ff * 12800);
+#pragma unroll
+        for (int i = 0; i < c1::OUT_PER_T; ++i) {
+            const int c = threadIdx.x + 256 * i;
+            pdy[i] = c < c1::OUT_CH ? __builtin_nontemporal_load(s + c) : u32x4{0, 0, 0, 0};
+        }
+    };
+    // tap geometry of this lane for the two k-tiles of this wave (k0 = 64w + 32t)
+    int toff[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const int tap = (64 * w + 32 * t) / 4 + 4 * (g & 1) + p;
+        const int ky = tap >> 3, kx = tap & 7;
+        toff[t] = ky * 84 + kx;  // pixel offset of the tap relative to (4oy, 4ox)
+    }
+    int f = blockIdx.x;
+    if (f < nframes) fetch(f);
+    for (; f < nframes; f += gridDim.x) {
+        c1_store_image(img, pre);
+#pragma unroll
+        for (int i = 0; i < c1::OUT_PER_T; ++i) {
+            const int c = threadIdx.x + 256 * i;
+            if (c < c1::OUT_CH) {
+                *(u32x4*)(dy + 16 * c) = pdy[i];
+                const bf16x8 v = __builtin_bit_cast(bf16x8, pdy[i]);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) csum[j] += (float)v[j];
+            }
+        }
+        const int fn = f + gridDim.x;
+        if (fn < nframes) fetch(fn);
+        __syncthreads();
+#pragma unroll 1
+        for (int ms = 0; ms < 25; ++ms) {
+            const int m_lo = ms * 16 + 8 * (g >> 1) + q;  // rows of the first tr read
+            const int m_hi = m_lo + 4;
+            const int oyl = m_lo / 20, oxl = m_lo - oyl * 20;
+            const int oyh = m_hi / 20, oxh = m_hi - oyh * 20;
+            const int pl = oyl * 4 * 84 + oxl * 4, ph = oyh * 4 * 84 + oxh * 4;  // pixel (x,y) base
+            // dY fragment: rows m, columns co = 16*(g&1) + 4p
+            const bf16x8 bfr = tr2(dy + m_lo * 64 + (16 * (g & 1) + 4 * p) * 2,
+                                   dy + m_hi * 64 + (16 * (g & 1) + 4 * p) * 2);
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const int xl = pl + toff[t], xh = ph + toff[t];
+                // pixel index P = y*84 + x -> pair qd = P/2 (x even <=> P even since 84 even)
+                const int yl = xl / 84, xxl = xl - yl * 84, yh = xh / 84, xxh = xh - yh * 84;
+                const char* al = img + ((xxl >> 1) & 1) * c1::PLANE + 16 * (yl * 21 + (xxl >> 2)) + 8 * (xxl & 1);
+                const char* ah = img + ((xxh >> 1) & 1) * c1::PLANE + 16 * (yh * 21 + (xxh >> 2)) + 8 * (xxh & 1);
+                const bf16x8 afr = tr2(al, ah);
+                if (t == 0) acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, bfr, acc0, 0, 0, 0);
+                else acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, bfr, acc1, 0, 0, 0);
+            }
+        }
+        __syncthreads();
+    }
+    // partial slab: rows k = 64w + 32t + (r&3) + 8(r>>2) + 4(lane>>5), col co = lane&31
+    float* out = slab + (size_t)blockIdx.x * 256 * 32;
+    const float inv255 = 1.0f / 255.0f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int k = 64 * w + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        out[k * 32 + (lane & 31)] = acc0[r] * inv255;
+        out[(k + 32) * 32 + (lane & 31)] = acc1[r] * inv255;
+    }
+    // bias partial: thread's chunks all have co octet = (threadIdx.x % 4) (256 % 4 == 0)
+    __syncthreads();
+    float* red = (float*)smem;  // [256][8]
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[threadIdx.x * 8 + j] = csum[j];
+    __syncthreads();
+    if (threadIdx.x < 32) {
+        const int oct = threadIdx.x >> 3, j = threadIdx.x & 7;
+        float s = 0.f;
+        for (int t = oct; t < 256; t += 4) s += red[t * 8 + j];
+        cs_slab[(size_t)blockIdx.x * 32 + threadIdx.x] = s;
+    }
+}
+
+int conv1_fwd_fr_launch(const uint8_t* frames, const __bf16* w1t, const float* bias, __bf16* a1,
+                        int nframes, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(conv1_fwd_fr, dim3(grid), dim3(256), 0, s, frames, w1t, bias, a1, nframes);
+    FI_HIP_CHECK(hipGetLastError());
+    return FI_OK;
+}
+
+int conv1_wgrad_fr_launch(const uint8_t* frames, const __bf16* da1, float* slab, float* cs_slab,
+                          int nframes, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(conv1_wgrad_fr, dim3(grid), dim3(256), 0, s, frames, da1, slab, cs_slab, nframes);
+    FI_HIP_CHECK(hipGetLastError());
+    return FI_OK;
+}
+
+}  // namespace fi

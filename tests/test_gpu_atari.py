@@ -107,3 +107,28 @@ def test_atari_publish_fits_actor_buffer():
     (reference cmd/freeimpala_mpi_*/main.cpp model size, agent.h:131-138)."""
     L = mk(T=1, B=16, publish="bf16")
     assert L.param_bytes == 2 * 1693875 <= 6 * 1024 * 1024
+
+
+def test_frame_resident_kernels_match_generic_path(monkeypatch):
+    """The frame-resident conv kernels and the generic implicit-GEMM path compute the same
+    layer (different fp32 summation order): activations within one bf16 ulp, grads 1e-4."""
+    T, B = 2, 16
+    outs = {}
+    for mode in ("generic", "fr"):
+        if mode == "generic":
+            monkeypatch.setenv("FI_ATARI_GENERIC", "1")
+        else:
+            monkeypatch.delenv("FI_ATARI_GENERIC", raising=False)
+        L = mk(T=T, B=B, seed=3)
+        L.synth(seed=77)
+        L.step_resident()
+        N = (T + 1) * B
+        outs[mode] = dict(a1=bf16_to_f32(L.tensor("a1", np.uint16, (N, 400 * 32))),
+                          da1=bf16_to_f32(L.tensor("da1", np.uint16, (N, 400 * 32))),
+                          g=L.tensor("grads"))
+        L.close()
+    a, b = outs["fr"], outs["generic"]
+    rel(a["a1"], b["a1"], "a1", l2=1e-3, mx=1e-2)
+    rel(a["da1"], b["da1"], "da1", l2=1e-3, mx=1e-2)
+    rel(a["g"][:8192], b["g"][:8192], "c1W", l2=1e-4, mx=1e-3)
+    rel(a["g"][8192:8224], b["g"][8192:8224], "c1b", l2=1e-4, mx=1e-3)
