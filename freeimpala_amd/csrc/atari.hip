@@ -530,6 +530,8 @@ int conv1_fwd_fr_launch(const uint8_t* frames, const __bf16* w1t, const float* b
                         int nframes, int grid, hipStream_t s);
 int conv1_wgrad_fr_launch(const uint8_t* frames, const __bf16* da1, float* slab, float* cs_slab,
                           int nframes, int grid, hipStream_t s);
+int conv2_bwd_fr_launch(const __bf16* a1, const __bf16* da2, const __bf16* w2d, __bf16* da1,
+                        float* slab, float* cs_slab, int nframes, int grid, hipStream_t s);
 constexpr int FR_GRID = 256;  // persistent frame-resident workgroups (1 per CU)
 
 static AtariImpl* impl(AtariNet* n) { return (AtariImpl*)n->impl; }
@@ -664,13 +666,20 @@ int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, con
                               ClassRows{I->wb.c3D, 64, C3K, I->cs3, (size_t)64 * C3K, nullptr},
                               EpiDgrad<9, 1>{I->da2, I->a2, N, I->cs3, 64}, I->cs3, 64, C3K, s)));
     // conv2: wgrad [512][64] + bias, dgrad -> da1 (4 parity classes, masked by a1)
-    FI_A("conv2_wgrad", (wgrad<128, 64, 2, 2>(ConvGather<20, 32, 4, 2, 9>{I->a1, N * P2}, RowsBf16{I->da2, N * P2, C2O},
+    if (I->fr) {
+        const int grid = std::min(N, FR_GRID);
+        FI_A("conv2_bwd", conv2_bwd_fr_launch(I->a1, I->da2, I->wb.c2D, I->da1, slab, cs, N, grid, s));
+        FI_A("reduce_slabs", reduce_slabs(slab, grid, (size_t)C2K * C2O, grads + o.c2w, s));
+        FI_A("reduce_slabs", reduce_slabs(cs, grid, (size_t)C2O, grads + o.c2b, s));
+    } else {
+        FI_A("conv2_wgrad", (wgrad<128, 64, 2, 2>(ConvGather<20, 32, 4, 2, 9>{I->a1, N * P2}, RowsBf16{I->da2, N * P2, C2O},
                                slab, cs, N * P2, C2K, C2O, SPL_C2, 1.f, s)));
-    FI_A("reduce_slabs", reduce_slabs(slab, SPL_C2, (size_t)C2K * C2O, grads + o.c2w, s));
-    FI_A("reduce_slabs", reduce_slabs(cs, SPL_C2, (size_t)C2O, grads + o.c2b, s));
-    FI_A("conv2_dgrad", (gemm<128, 32, 4, 1>(DgradGather<20, 4, 2, 9, 64>{I->da2, N, I->cs2},
+        FI_A("reduce_slabs", reduce_slabs(slab, SPL_C2, (size_t)C2K * C2O, grads + o.c2w, s));
+        FI_A("reduce_slabs", reduce_slabs(cs, SPL_C2, (size_t)C2O, grads + o.c2b, s));
+        FI_A("conv2_dgrad", (gemm<128, 32, 4, 1>(DgradGather<20, 4, 2, 9, 64>{I->da2, N, I->cs2},
                               ClassRows{I->wb.c2D, 32, 256, I->cs2, (size_t)32 * 256, nullptr},
                               EpiDgrad<20, 2>{I->da1, I->a1, N, I->cs2, 32}, 4 * I->cs2, 32, 256, s)));
+    }
     // conv1: wgrad [256][32] (+1/255 input scale) + bias
     if (I->fr) {
         const int grid = std::min(N, FR_GRID);

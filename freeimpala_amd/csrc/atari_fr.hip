@@ -244,4 +244,226 @@ int conv1_wgrad_fr_launch(const uint8_t* frames, const __bf16* da1, float* slab,
     return FI_OK;
 }
 
+
+// =====================================================================================
+// conv2 backward, fused and frame-resident (4x4 / stride 2, 32 -> 64 channels, 20x20 -> 9x9)
+//   in : X = a1[f] (20,20,32) bf16 (layer input = ReLU mask),  dY = da2[f] (9,9,64) bf16
+//   out: da1[f] = (X > 0) * dgrad(dY, W2)   (written in place over X in LDS, then stored)
+//        dW2 += im2col(X)^T dY  (512 x 64, registers across frames),  db2 += sum dY
+// LDS ring of 3 frames, filled by LDS-DMA (global_load_lds_dwordx4), counted vmcnt.
+//   X image : pixel p at 256*(p>>2) + 64*sigma(p), sigma(p) = ((p&3) + ((p>>2)&1)) & 3
+//             -> the four stride-2 pixels a transposed read gathers sit in different
+//                quarters of a 256-byte bank row (conflict-free ds_read_b64_tr_b16)
+//   dY tile : row r (output pixel) at 128*r, 16-byte chunk c at 16*(c ^ f(r)),
+//             f(r) = (((r>>1)&1)<<2) | ((r>>2)&3): conflict-free both for the b128 row
+//             reads of the dgrad and the transposed reads of the wgrad.
+// wgrad: wave w owns taps (ky=w, kx=0..3) = k rows [128w, 128w+128) x 64 co.
+// dgrad: wave w owns parity class (py, px) = (w>>1, w&1): 100 input pixels (4 row tiles),
+//        K = (ty, tx, co) = 256, W2 class slice kept in registers (64 VGPRs).
+// =====================================================================================
+namespace c2 {
+constexpr int XB = 20 * 20 * 32 * 2;         // 25,600
+constexpr int DYROWS = 96;                   // 81 rows padded to 6 MFMA K-steps
+constexpr int DYB = DYROWS * 128;            // 12,288
+constexpr int SLOT = XB + DYB;               // 37,888
+constexpr int RING = 3;
+constexpr int NX = XB / 1024;                // 25 LDS-DMA pieces (1 KiB each)
+constexpr int NDY = DYB / 1024;              // 12
+constexpr int NPIECE = NX + NDY;             // 37
+constexpr int OUT_CH = XB / 16;              // 1600 16-byte chunks of da1
+}  // namespace c2
+
+__device__ __forceinline__ int c2_sigma(int p) { return ((p & 3) + ((p >> 2) & 1)) & 3; }
+__device__ __forceinline__ int c2_xaddr(int p) { return 256 * (p >> 2) + 64 * c2_sigma(p); }
+__device__ __forceinline__ int c2_f(int r) { return (((r >> 1) & 1) << 2) | ((r >> 2) & 3); }
+__device__ __forceinline__ int c2_dyaddr(int r, int c) { return 128 * r + 16 * (c ^ c2_f(r)); }
+
+__device__ __forceinline__ void c2_issue(const __bf16* x, const __bf16* dy, uint32_t slot_lds,
+                                         int w, int lane) {
+#pragma unroll
+    for (int i = 0; i < (c2::NPIECE + 3) / 4; ++i) {
+        const int j = w + 4 * i;
+        if (j >= c2::NPIECE) break;
+        if (j < c2::NX) {
+            const int P = j * 64 + lane;  // physical 16-byte piece of the X image
+            const int G = P >> 4, s = (P >> 2) & 3, c = P & 3;
+            const int p = 4 * G + ((s - (G & 1)) & 3);
+            glds16((const char*)x + p * 64 + c * 16, slot_lds + j * 1024);
+        } else {
+            const int P = (j - c2::NX) * 64 + lane;  // physical piece of the dY tile
+            const int r = P >> 3, pc = P & 7;
+            const int rs = r < 81 ? r : 80;
+            glds16((const char*)dy + rs * 128 + 16 * (pc ^ c2_f(r)), slot_lds + c2::XB + (j - c2::NX) * 1024);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256, 1) void conv2_bwd_fr(const __bf16* __restrict__ a1,
+                                                       const __bf16* __restrict__ da2,
+                                                       const __bf16* __restrict__ w2d,  // [4][32][256]
+                                                       __bf16* __restrict__ da1,
+                                                       float* __restrict__ slab,   // [grid][512][64]
+                                                       float* __restrict__ cs_slab,  // [grid][64]
+                                                       int nframes) {
+    __shared__ __attribute__((aligned(16))) char smem[c2::RING * c2::SLOT];
+    const int lane = threadIdx.x & 63;
+    const int w = wave_id();
+    const int g = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3, h = lane >> 5, col = lane & 31;
+    const uint32_t lds0 = lds_addr(smem);
+
+    // dgrad B fragments (class w): W[k = 16ks + 8h + j][ci = col]
+    bf16x8 bw[16];
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) bw[ks] = *(const bf16x8*)(w2d + ((size_t)(w * 32 + col)) * 256 + ks * 16 + h * 8);
+    const int py = w >> 1, px = w & 1;
+
+    f32x16 accw[4][2];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) { accw[t][0] = f32x16{}; accw[t][1] = f32x16{}; }
+    float bsum0 = 0.f, bsum1 = 0.f;
+
+    const int npw = (c2::NPIECE - w + 3) / 4;  // LDS-DMA pieces per wave per frame
+    constexpr int STORES = c2::OUT_CH / 256;   // 6 store instructions every wave surely issues
+    int issued = 0, m0 = 0, m1 = 0, m2 = 0;
+    const int nmine = nframes > (int)blockIdx.x ? (nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+    for (int i = 0; i < 3 && i < nmine; ++i) {
+        const int f = blockIdx.x + i * gridDim.x;
+        c2_issue(a1 + (size_t)f * 12800, da2 + (size_t)f * 5184, lds0 + i * c2::SLOT, w, lane);
+        issued += npw;
+        if (i == 0) m0 = issued; else if (i == 1) m1 = issued; else m2 = issued;
+    }
+    for (int it = 0; it < nmine; ++it) {
+        const int f = blockIdx.x + it * gridDim.x;
+        const int slot = it % 3;
+        char* X = smem + slot * c2::SLOT;
+        const char* DY = X + c2::XB;
+        wait_vmcnt(issued - m0);
+        lds_barrier();
+
+        // ---------------- weight gradient: A^T = im2col(X) (tr reads), B = dY (tr reads)
+#pragma unroll 1
+        for (int ms = 0; ms < 6; ++ms) {
+            const int mlo = ms * 16 + 8 * (g >> 1) + q, mhi = mlo + 4;
+            bf16x8 bfr[2];
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct) {
+                const int c = 4 * ct + 2 * (g & 1) + (p4 >> 1);
+                const int off = 8 * (p4 & 1);
+                const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(DY + c2_dyaddr(mlo, c) + off));
+                const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(DY + c2_dyaddr(mhi, c) + off));
+                bf16x8 v = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                const int mb = ms * 16 + 8 * (g >> 1);  // element j <-> m = mb + j
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (mb + j >= 81) v[j] = (__bf16)0.f;
+                bfr[ct] = v;
+                if (w == 0) {
+                    float s = 0.f;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) s += (float)v[j];
+                    if (ct == 0) bsum0 += s; else bsum1 += s;
+                }
+            }
+            const int ml = min(mlo, 80), mh = min(mhi, 80);
+            const int oyl = ml / 9, oxl = ml - oyl * 9, oyh = mh / 9, oxh = mh - oyh * 9;
+            const int ci = 16 * (g & 1) + 4 * p4;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {  // tap (ky = w, kx = t)
+                const int pl = (2 * oyl + w) * 20 + 2 * oxl + t, ph = (2 * oyh + w) * 20 + 2 * oxh + t;
+                const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(X + c2_xaddr(pl) + 2 * ci));
+                const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(X + c2_xaddr(ph) + 2 * ci));
+                const bf16x8 afr = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                accw[t][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, bfr[0], accw[t][0], 0, 0, 0);
+                accw[t][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, bfr[1], accw[t][1], 0, 0, 0);
+            }
+        }
+
+        // ---------------- data gradient of class (py, px): rows = 100 input pixels
+        f32x16 accd[4];
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt) {
+            const int r = min(rt * 32 + col, 99);
+            const int iyq = r / 10, ixq = r - iyq * 10;
+            f32x16 acc = {};
+#pragma unroll
+            for (int ks = 0; ks < 16; ++ks) {
+                const int tap = ks >> 2, ty = tap >> 1, tx = tap & 1;
+                const int oy = iyq - ty, ox = ixq - tx;
+                const bool ok = oy >= 0 && ox >= 0 && oy < 9 && ox < 9;
+                const int row = ok ? oy * 9 + ox : 0;
+                const int c = 2 * (ks & 3) + h;  // co chunk: co0 = 16*(ks%4) + 8h
+                bf16x8 a = *(const bf16x8*)(DY + c2_dyaddr(row, c));
+                if (!ok) a = bf16x8{};
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bw[ks], acc, 0, 0, 0);
+            }
+            accd[rt] = acc;
+        }
+        lds_barrier();  // every wave done reading X (wgrad) before the in-place da1 write
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int ri = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (ri < 100) {
+                    const int iy = 2 * (ri / 10) + py, ix = 2 * (ri % 10) + px;
+                    __bf16* e = (__bf16*)(X + c2_xaddr(iy * 20 + ix)) + col;
+                    *e = (float)*e > 0.f ? (__bf16)accd[rt][r] : (__bf16)0.f;
+                }
+            }
+        lds_barrier();  // da1 tile complete
+        {
+            u32x4* dst = (u32x4*)(da1 + (size_t)f * 12800);
+#pragma unroll
+            for (int i = 0; i < (c2::OUT_CH + 255) / 256; ++i) {
+                const int P = threadIdx.x + 256 * i;
+                if (P < c2::OUT_CH) {
+                    const int G = P >> 4, s = (P >> 2) & 3, c = P & 3;
+                    const int pp = 4 * G + ((s - (G & 1)) & 3);
+                    __builtin_nontemporal_store(*(const u32x4*)(X + 16 * P), dst + pp * 4 + c);
+                }
+            }
+            issued += STORES;  // (wave 0 issues one more; counting fewer only waits longer)
+        }
+        lds_barrier();  // slot fully consumed
+        int m3 = 0;
+        if (it + 3 < nmine) {
+            const int fn = blockIdx.x + (it + 3) * gridDim.x;
+            c2_issue(a1 + (size_t)fn * 12800, da2 + (size_t)fn * 5184, lds0 + slot * c2::SLOT, w, lane);
+            issued += npw;
+            m3 = issued;
+        }
+        m0 = m1;
+        m1 = m2;
+        m2 = m3;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // weight-gradient partial: k = 128w + 32t + row, co = 32ct + col
+    float* out = slab + (size_t)blockIdx.x * 512 * 64;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int k = 128 * w + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
+                out[k * 64 + 32 * ct + col] = accw[t][ct][r];
+            }
+    // bias: wave 0 lanes l and l+32 hold the same co (16*(g&1) + (l&15)), different m halves
+    if (w == 0) {
+        const float o0 = __shfl_xor(bsum0, 32, 64), o1 = __shfl_xor(bsum1, 32, 64);
+        if (lane < 32) {
+            cs_slab[(size_t)blockIdx.x * 64 + lane] = bsum0 + o0;
+            cs_slab[(size_t)blockIdx.x * 64 + 32 + lane] = bsum1 + o1;
+        }
+    }
+}
+
+int conv2_bwd_fr_launch(const __bf16* a1, const __bf16* da2, const __bf16* w2d, __bf16* da1,
+                        float* slab, float* cs_slab, int nframes, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(conv2_bwd_fr, dim3(grid), dim3(256), 0, s, a1, da2, w2d, da1, slab, cs_slab,
+                       nframes);
+    FI_HIP_CHECK(hipGetLastError());
+    return FI_OK;
+}
+
 }  // namespace fi
