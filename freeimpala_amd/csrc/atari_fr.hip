@@ -166,6 +166,24 @@ __global__ __launch_bounds__(256, 1) void conv1_wgrad_fr(const uint8_t* __restri
         const int ky = tap >> 3, kx = tap & 7;
         toff[t] = ky * 84 + kx;  // pixel offset of the tap relative to (4oy, 4ox)
     }
+    // frame-invariant per-lane LDS offsets of every transposed read: A [ms][t][lo/hi], B [ms][lo/hi]
+    int wao[25][2][2], wbo[25][2];
+#pragma unroll
+    for (int ms = 0; ms < 25; ++ms) {
+        const int m_lo = ms * 16 + 8 * (g >> 1) + q;
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            const int m = m_lo + 4 * hh;
+            const int oy = m / 20, ox = m - oy * 20;
+            wbo[ms][hh] = m * 64 + (16 * (g & 1) + 4 * p) * 2;
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const int P = oy * 4 * 84 + ox * 4 + toff[t];
+                const int y = P / 84, x = P - y * 84;
+                wao[ms][t][hh] = ((x >> 1) & 1) * c1::PLANE + 16 * (y * 21 + (x >> 2)) + 8 * (x & 1);
+            }
+        }
+    }
     int f = blockIdx.x;
     if (f < nframes) fetch(f);
     for (; f < nframes; f += gridDim.x) {
@@ -183,27 +201,11 @@ __global__ __launch_bounds__(256, 1) void conv1_wgrad_fr(const uint8_t* __restri
         const int fn = f + gridDim.x;
         if (fn < nframes) fetch(fn);
         __syncthreads();
-#pragma unroll 1
-        for (int ms = 0; ms < 25; ++ms) {
-            const int m_lo = ms * 16 + 8 * (g >> 1) + q;  // rows of the first tr read
-            const int m_hi = m_lo + 4;
-            const int oyl = m_lo / 20, oxl = m_lo - oyl * 20;
-            const int oyh = m_hi / 20, oxh = m_hi - oyh * 20;
-            const int pl = oyl * 4 * 84 + oxl * 4, ph = oyh * 4 * 84 + oxh * 4;  // pixel (x,y) base
-            // dY fragment: rows m, columns co = 16*(g&1) + 4p
-            const bf16x8 bfr = tr2(dy + m_lo * 64 + (16 * (g & 1) + 4 * p) * 2,
-                                   dy + m_hi * 64 + (16 * (g & 1) + 4 * p) * 2);
 #pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                const int xl = pl + toff[t], xh = ph + toff[t];
-                // pixel index P = y*84 + x -> pair qd = P/2 (x even <=> P even since 84 even)
-                const int yl = xl / 84, xxl = xl - yl * 84, yh = xh / 84, xxh = xh - yh * 84;
-                const char* al = img + ((xxl >> 1) & 1) * c1::PLANE + 16 * (yl * 21 + (xxl >> 2)) + 8 * (xxl & 1);
-                const char* ah = img + ((xxh >> 1) & 1) * c1::PLANE + 16 * (yh * 21 + (xxh >> 2)) + 8 * (xxh & 1);
-                const bf16x8 afr = tr2(al, ah);
-                if (t == 0) acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, bfr, acc0, 0, 0, 0);
-                else acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, bfr, acc1, 0, 0, 0);
-            }
+        for (int ms = 0; ms < 25; ++ms) {
+            const bf16x8 bfr = tr2(dy + wbo[ms][0], dy + wbo[ms][1]);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr2(img + wao[ms][0][0], img + wao[ms][0][1]), bfr, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr2(img + wao[ms][1][0], img + wao[ms][1][1]), bfr, acc1, 0, 0, 0);
         }
         __syncthreads();
     }
@@ -316,12 +318,52 @@ __global__ __launch_bounds__(256, 1) void conv2_bwd_fr(const __bf16* __restrict_
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks) bw[ks] = *(const bf16x8*)(w2d + ((size_t)(w * 32 + col)) * 256 + ks * 16 + h * 8);
     const int py = w >> 1, px = w & 1;
-
     f32x16 accw[4][2];
 #pragma unroll
     for (int t = 0; t < 4; ++t) { accw[t][0] = f32x16{}; accw[t][1] = f32x16{}; }
     float bsum0 = 0.f, bsum1 = 0.f;
 
+    // ---- frame-invariant LDS addresses (byte offsets inside a ring slot), per lane
+    // wgrad B (dY, tr reads): [ms][ct][lo/hi]
+    int wb_addr[6][2][2];
+    // wgrad A (X image, tr reads): [ms][tap kx][lo/hi]
+    int wa_addr[6][4][2];
+#pragma unroll
+    for (int ms = 0; ms < 6; ++ms) {
+        const int mlo = ms * 16 + 8 * (g >> 1) + q, mhi = mlo + 4;
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {
+            const int c = 4 * ct + 2 * (g & 1) + (p4 >> 1);
+            wb_addr[ms][ct][0] = c2::XB + c2_dyaddr(mlo, c) + 8 * (p4 & 1);
+            wb_addr[ms][ct][1] = c2::XB + c2_dyaddr(mhi, c) + 8 * (p4 & 1);
+        }
+        const int ml = min(mlo, 80), mh = min(mhi, 80);
+        const int oyl = ml / 9, oxl = ml - oyl * 9, oyh = mh / 9, oxh = mh - oyh * 9;
+        const int ci = 16 * (g & 1) + 4 * p4;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            wa_addr[ms][t][0] = c2_xaddr((2 * oyl + w) * 20 + 2 * oxl + t) + 2 * ci;
+            wa_addr[ms][t][1] = c2_xaddr((2 * oyh + w) * 20 + 2 * oxh + t) + 2 * ci;
+        }
+    }
+    // lanes whose B rows m = 80 + 8*(g>>1) + j pass 81 in the last K-step get zeroed there
+    const int mb5 = 80 + 8 * (g >> 1);
+    // dgrad A (dY rows, b128): [rt][ks] address and validity bit
+    int da_addr[4][16];
+    uint64_t da_ok = 0;
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt) {
+        const int r = min(rt * 32 + col, 99);
+        const int iyq = r / 10, ixq = r - iyq * 10;
+#pragma unroll
+        for (int ks = 0; ks < 16; ++ks) {
+            const int tap = ks >> 2, ty = tap >> 1, tx = tap & 1;
+            const int oy = iyq - ty, ox = ixq - tx;
+            const bool ok = oy >= 0 && ox >= 0 && oy < 9 && ox < 9;
+            da_addr[rt][ks] = c2::XB + c2_dyaddr(ok ? oy * 9 + ox : 0, 2 * (ks & 3) + h);
+            if (ok) da_ok |= 1ull << (rt * 16 + ks);
+        }
+    }
     const int npw = (c2::NPIECE - w + 3) / 4;  // LDS-DMA pieces per wave per frame
     constexpr int STORES = c2::OUT_CH / 256;   // 6 store instructions every wave surely issues
     int issued = 0, m0 = 0, m1 = 0, m2 = 0;
@@ -336,80 +378,58 @@ __global__ __launch_bounds__(256, 1) void conv2_bwd_fr(const __bf16* __restrict_
         const int f = blockIdx.x + it * gridDim.x;
         const int slot = it % 3;
         char* X = smem + slot * c2::SLOT;
-        const char* DY = X + c2::XB;
         wait_vmcnt(issued - m0);
         lds_barrier();
 
         // ---------------- weight gradient: A^T = im2col(X) (tr reads), B = dY (tr reads)
-#pragma unroll 1
+#pragma unroll
         for (int ms = 0; ms < 6; ++ms) {
-            const int mlo = ms * 16 + 8 * (g >> 1) + q, mhi = mlo + 4;
             bf16x8 bfr[2];
 #pragma unroll
             for (int ct = 0; ct < 2; ++ct) {
-                const int c = 4 * ct + 2 * (g & 1) + (p4 >> 1);
-                const int off = 8 * (p4 & 1);
-                const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(DY + c2_dyaddr(mlo, c) + off));
-                const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(DY + c2_dyaddr(mhi, c) + off));
-                bf16x8 v = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                const int mb = ms * 16 + 8 * (g >> 1);  // element j <-> m = mb + j
+                bf16x8 v = tr2(X + wb_addr[ms][ct][0], X + wb_addr[ms][ct][1]);
+                if (ms == 5) {
 #pragma unroll
-                for (int j = 0; j < 8; ++j)
-                    if (mb + j >= 81) v[j] = (__bf16)0.f;
+                    for (int j = 0; j < 8; ++j)
+                        if (mb5 + j >= 81) v[j] = (__bf16)0.f;
+                }
                 bfr[ct] = v;
                 if (w == 0) {
-                    float s = 0.f;
+                    float sacc = 0.f;
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) s += (float)v[j];
-                    if (ct == 0) bsum0 += s; else bsum1 += s;
+                    for (int j = 0; j < 8; ++j) sacc += (float)v[j];
+                    if (ct == 0) bsum0 += sacc; else bsum1 += sacc;
                 }
             }
-            const int ml = min(mlo, 80), mh = min(mhi, 80);
-            const int oyl = ml / 9, oxl = ml - oyl * 9, oyh = mh / 9, oxh = mh - oyh * 9;
-            const int ci = 16 * (g & 1) + 4 * p4;
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {  // tap (ky = w, kx = t)
-                const int pl = (2 * oyl + w) * 20 + 2 * oxl + t, ph = (2 * oyh + w) * 20 + 2 * oxh + t;
-                const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(X + c2_xaddr(pl) + 2 * ci));
-                const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(X + c2_xaddr(ph) + 2 * ci));
-                const bf16x8 afr = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            for (int t = 0; t < 4; ++t) {
+                const bf16x8 afr = tr2(X + wa_addr[ms][t][0], X + wa_addr[ms][t][1]);
                 accw[t][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, bfr[0], accw[t][0], 0, 0, 0);
                 accw[t][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, bfr[1], accw[t][1], 0, 0, 0);
             }
         }
+        lds_barrier();  // every wave done reading X before the in-place da1 writes
 
         // ---------------- data gradient of class (py, px): rows = 100 input pixels
-        f32x16 accd[4];
 #pragma unroll
         for (int rt = 0; rt < 4; ++rt) {
-            const int r = min(rt * 32 + col, 99);
-            const int iyq = r / 10, ixq = r - iyq * 10;
             f32x16 acc = {};
 #pragma unroll
             for (int ks = 0; ks < 16; ++ks) {
-                const int tap = ks >> 2, ty = tap >> 1, tx = tap & 1;
-                const int oy = iyq - ty, ox = ixq - tx;
-                const bool ok = oy >= 0 && ox >= 0 && oy < 9 && ox < 9;
-                const int row = ok ? oy * 9 + ox : 0;
-                const int c = 2 * (ks & 3) + h;  // co chunk: co0 = 16*(ks%4) + 8h
-                bf16x8 a = *(const bf16x8*)(DY + c2_dyaddr(row, c));
-                if (!ok) a = bf16x8{};
+                bf16x8 a = *(const bf16x8*)(X + da_addr[rt][ks]);
+                if (!((da_ok >> (rt * 16 + ks)) & 1)) a = bf16x8{};
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bw[ks], acc, 0, 0, 0);
             }
-            accd[rt] = acc;
-        }
-        lds_barrier();  // every wave done reading X (wgrad) before the in-place da1 write
-#pragma unroll
-        for (int rt = 0; rt < 4; ++rt)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int ri = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
                 if (ri < 100) {
                     const int iy = 2 * (ri / 10) + py, ix = 2 * (ri % 10) + px;
                     __bf16* e = (__bf16*)(X + c2_xaddr(iy * 20 + ix)) + col;
-                    *e = (float)*e > 0.f ? (__bf16)accd[rt][r] : (__bf16)0.f;
+                    *e = (float)*e > 0.f ? (__bf16)acc[r] : (__bf16)0.f;
                 }
             }
+        }
         lds_barrier();  // da1 tile complete
         {
             u32x4* dst = (u32x4*)(da1 + (size_t)f * 12800);
