@@ -22,8 +22,11 @@ def atari_kernel_work(T: int, B: int, A: int) -> dict:
         "conv3_wgrad": ("flop", c3), "conv3_dgrad": ("flop", c3),
         "conv2_wgrad": ("flop", c2), "conv2_dgrad": ("flop", c2),
         "conv1_wgrad": ("flop", c1),
+        # fused frame-resident backward kernels: wgrad + dgrad of the layer in one launch
+        "conv2_bwd": ("flop", 2 * c2), "conv3_bwd": ("flop", 2 * c3),
     }
 
 
 def atari_step_flops(T: int, B: int, A: int) -> int:
-    return sum(v for _, v in atari_kernel_work(T, B, A).values())
+    w = atari_kernel_work(T, B, A)
+    return sum(v for k, (_, v) in w.items() if not k.endswith("_bwd"))

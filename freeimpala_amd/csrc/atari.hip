@@ -532,6 +532,8 @@ int conv1_wgrad_fr_launch(const uint8_t* frames, const __bf16* da1, float* slab,
                           int nframes, int grid, hipStream_t s);
 int conv2_bwd_fr_launch(const __bf16* a1, const __bf16* da2, const __bf16* w2d, __bf16* da1,
                         float* slab, float* cs_slab, int nframes, int grid, hipStream_t s);
+int conv3_bwd_fr_launch(const __bf16* a2, const __bf16* da3, const __bf16* w3d, __bf16* da2,
+                        float* slab, float* cs_slab, int nframes, int grid, hipStream_t s);
 constexpr int FR_GRID = 256;  // persistent frame-resident workgroups (1 per CU)
 
 static AtariImpl* impl(AtariNet* n) { return (AtariImpl*)n->impl; }
@@ -658,13 +660,20 @@ int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, con
     FI_A("fc_dgrad", (gemm<128, 128, 2, 2>(RowsBf16{I->dh, N, FCO}, RowsBf16{I->wb.fcB, FCK, FCO},
                                EpiMaskBf16{I->da3, I->a3, FCK}, N, FCK, FCO, s)));
     // conv3: wgrad [576][64] + bias, dgrad -> da2 (masked by a2)
-    FI_A("conv3_wgrad", (wgrad<128, 64, 2, 2>(ConvGather<9, 64, 3, 1, 7>{I->a2, N * P3}, RowsBf16{I->da3, N * P3, C3O},
-                               slab, cs, N * P3, C3K, C3O, SPL_C3, 1.f, s)));
-    FI_A("reduce_slabs", reduce_slabs(slab, SPL_C3, (size_t)C3K * C3O, grads + o.c3w, s));
-    FI_A("reduce_slabs", reduce_slabs(cs, SPL_C3, (size_t)C3O, grads + o.c3b, s));
-    FI_A("conv3_dgrad", (gemm<128, 64, 2, 2>(DgradGather<9, 3, 1, 7, 64>{I->da3, N, I->cs3},
-                              ClassRows{I->wb.c3D, 64, C3K, I->cs3, (size_t)64 * C3K, nullptr},
-                              EpiDgrad<9, 1>{I->da2, I->a2, N, I->cs3, 64}, I->cs3, 64, C3K, s)));
+    if (I->fr) {
+        const int grid = std::min(N, FR_GRID);
+        FI_A("conv3_bwd", conv3_bwd_fr_launch(I->a2, I->da3, I->wb.c3D, I->da2, slab, cs, N, grid, s));
+        FI_A("reduce_slabs", reduce_slabs(slab, grid, (size_t)C3K * C3O, grads + o.c3w, s));
+        FI_A("reduce_slabs", reduce_slabs(cs, grid, (size_t)C3O, grads + o.c3b, s));
+    } else {
+        FI_A("conv3_wgrad", (wgrad<128, 64, 2, 2>(ConvGather<9, 64, 3, 1, 7>{I->a2, N * P3}, RowsBf16{I->da3, N * P3, C3O},
+                                   slab, cs, N * P3, C3K, C3O, SPL_C3, 1.f, s)));
+        FI_A("reduce_slabs", reduce_slabs(slab, SPL_C3, (size_t)C3K * C3O, grads + o.c3w, s));
+        FI_A("reduce_slabs", reduce_slabs(cs, SPL_C3, (size_t)C3O, grads + o.c3b, s));
+        FI_A("conv3_dgrad", (gemm<128, 64, 2, 2>(DgradGather<9, 3, 1, 7, 64>{I->da3, N, I->cs3},
+                                  ClassRows{I->wb.c3D, 64, C3K, I->cs3, (size_t)64 * C3K, nullptr},
+                                  EpiDgrad<9, 1>{I->da2, I->a2, N, I->cs3, 64}, I->cs3, 64, C3K, s)));
+    }
     // conv2: wgrad [512][64] + bias, dgrad -> da1 (4 parity classes, masked by a1)
     if (I->fr) {
         const int grid = std::min(N, FR_GRID);

@@ -273,6 +273,7 @@ constexpr int NX = XB / 1024;                // 25 LDS-DMA pieces (1 KiB each)
 constexpr int NDY = DYB / 1024;              // 12
 constexpr int NPIECE = NX + NDY;             // 37
 constexpr int OUT_CH = XB / 16;              // 1600 16-byte chunks of da1
+constexpr int OUTT = 4 * 128 * 32 * 2;       // 32 KiB dgrad tile in accumulator order
 }  // namespace c2
 
 __device__ __forceinline__ int c2_sigma(int p) { return ((p & 3) + ((p >> 2) & 1)) & 3; }
@@ -307,17 +308,17 @@ __global__ __launch_bounds__(256, 1) void conv2_bwd_fr(const __bf16* __restrict_
                                                        float* __restrict__ slab,   // [grid][512][64]
                                                        float* __restrict__ cs_slab,  // [grid][64]
                                                        int nframes) {
-    __shared__ __attribute__((aligned(16))) char smem[c2::RING * c2::SLOT];
+    __shared__ __attribute__((aligned(16))) char smem[c2::RING * c2::SLOT + c2::OUTT];
     const int lane = threadIdx.x & 63;
     const int w = wave_id();
     const int g = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3, h = lane >> 5, col = lane & 31;
+    __bf16* outt = (__bf16*)(smem + c2::RING * c2::SLOT);  // [cls][128][32], unmasked dX
     const uint32_t lds0 = lds_addr(smem);
 
     // dgrad B fragments (class w): W[k = 16ks + 8h + j][ci = col]
     bf16x8 bw[16];
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks) bw[ks] = *(const bf16x8*)(w2d + ((size_t)(w * 32 + col)) * 256 + ks * 16 + h * 8);
-    const int py = w >> 1, px = w & 1;
     f32x16 accw[4][2];
 #pragma unroll
     for (int t = 0; t < 4; ++t) { accw[t][0] = f32x16{}; accw[t][1] = f32x16{}; }
@@ -408,7 +409,6 @@ __global__ __launch_bounds__(256, 1) void conv2_bwd_fr(const __bf16* __restrict_
                 accw[t][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, bfr[1], accw[t][1], 0, 0, 0);
             }
         }
-        lds_barrier();  // every wave done reading X before the in-place da1 writes
 
         // ---------------- data gradient of class (py, px): rows = 100 input pixels
 #pragma unroll
@@ -423,23 +423,25 @@ __global__ __launch_bounds__(256, 1) void conv2_bwd_fr(const __bf16* __restrict_
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int ri = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (ri < 100) {
-                    const int iy = 2 * (ri / 10) + py, ix = 2 * (ri % 10) + px;
-                    __bf16* e = (__bf16*)(X + c2_xaddr(iy * 20 + ix)) + col;
-                    *e = (float)*e > 0.f ? (__bf16)acc[r] : (__bf16)0.f;
-                }
+                outt[(w * 128 + ri) * 32 + col] = (__bf16)acc[r];
             }
         }
-        lds_barrier();  // da1 tile complete
-        {
+        lds_barrier();  // dgrad tile complete
+        {  // da1 = (X > 0) * dX, in NHWC order: chunk P = pixel P/4, channels 8*(P%4)..+8
             u32x4* dst = (u32x4*)(da1 + (size_t)f * 12800);
 #pragma unroll
             for (int i = 0; i < (c2::OUT_CH + 255) / 256; ++i) {
                 const int P = threadIdx.x + 256 * i;
                 if (P < c2::OUT_CH) {
-                    const int G = P >> 4, s = (P >> 2) & 3, c = P & 3;
-                    const int pp = 4 * G + ((s - (G & 1)) & 3);
-                    __builtin_nontemporal_store(*(const u32x4*)(X + 16 * P), dst + pp * 4 + c);
+                    const int pix = P >> 2, c = P & 3;
+                    const int iy = pix / 20, ix = pix - iy * 20;
+                    const int cls = ((iy & 1) << 1) | (ix & 1), ri = (iy >> 1) * 10 + (ix >> 1);
+                    const bf16x8 v = *(const bf16x8*)(outt + (cls * 128 + ri) * 32 + 8 * c);
+                    const bf16x8 m = *(const bf16x8*)(X + c2_xaddr(pix) + 16 * c);
+                    bf16x8 o;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) o[j] = (float)m[j] > 0.f ? v[j] : (__bf16)0.f;
+                    __builtin_nontemporal_store(__builtin_bit_cast(u32x4, o), dst + P);
                 }
             }
             issued += STORES;  // (wave 0 issues one more; counting fewer only waits longer)
@@ -481,6 +483,258 @@ __global__ __launch_bounds__(256, 1) void conv2_bwd_fr(const __bf16* __restrict_
 int conv2_bwd_fr_launch(const __bf16* a1, const __bf16* da2, const __bf16* w2d, __bf16* da1,
                         float* slab, float* cs_slab, int nframes, int grid, hipStream_t s) {
     hipLaunchKernelGGL(conv2_bwd_fr, dim3(grid), dim3(256), 0, s, a1, da2, w2d, da1, slab, cs_slab,
+                       nframes);
+    FI_HIP_CHECK(hipGetLastError());
+    return FI_OK;
+}
+
+
+// =====================================================================================
+// conv3 backward, fused and frame-resident (3x3 / stride 1, 64 -> 64 channels, 9x9 -> 7x7)
+//   in : X = a2[f] (9,9,64), dY = da3[f] (7,7,64);  out: da2[f] = (X>0) * dgrad(dY, W3),
+//        dW3 (576 x 64) and db3 accumulated in registers across frames.
+// X image : pixel p at 128p, its 64-byte channel halves swapped when (p>>1)&1 -> the four
+//           consecutive pixels of a transposed read land in distinct bank quarters.
+// dY tile : 64 rows (49 valid) x 128 B, chunk swizzle c ^ f(r) as in conv2.
+// wgrad: 32x32x16 MFMA, k-tile kt = (tap, 32-channel half), waves take kt = w, w+4, ...
+// dgrad: 16x16x32 MFMA, wave w owns input channels 16w..16w+15 for all 6 row tiles of 16
+//        input pixels; its W3 slice (18 K-steps) lives in registers; taps that fall
+//        outside the 7x7 output read a 16-byte zero row instead of being masked.
+// =====================================================================================
+namespace c3 {
+constexpr int XB = 11 * 1024;                // 81 px * 128 B = 10,368, padded to 11 KiB
+constexpr int DYB = 64 * 128;                // 8 KiB
+constexpr int SLOT = XB + DYB;               // 19,456
+constexpr int RING = 3;
+constexpr int NX = 11, NDY = 8, NPIECE = NX + NDY;   // 19 LDS-DMA pieces
+constexpr int OUTT = 96 * 128;               // dgrad tile [96 rows][64 ci] bf16
+constexpr int ZERO = 64;                     // zero row (16 B used)
+constexpr int OUT_CH = 81 * 8;               // 648 16-byte chunks of da2
+}  // namespace c3
+
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int c3_xaddr(int p, int ci) {  // byte offset of (pixel, channel)
+    return 128 * p + 64 * ((ci >> 5) ^ ((p >> 1) & 1)) + 2 * (ci & 31);
+}
+
+__device__ __forceinline__ void c3_issue(const __bf16* x, const __bf16* dy, uint32_t slot_lds,
+                                         int w, int lane) {
+#pragma unroll
+    for (int i = 0; i < (c3::NPIECE + 3) / 4; ++i) {
+        const int j = w + 4 * i;
+        if (j >= c3::NPIECE) break;
+        if (j < c3::NX) {
+            const int P = j * 64 + lane;         // physical 16-byte piece of the X image
+            const int p = min(P >> 3, 80), pc = P & 7;
+            const int lc = 4 * ((pc >> 2) ^ ((p >> 1) & 1)) + (pc & 3);  // logical chunk
+            glds16((const char*)x + p * 128 + 16 * lc, slot_lds + j * 1024);
+        } else {
+            const int P = (j - c3::NX) * 64 + lane;
+            const int r = P >> 3, pc = P & 7;
+            const int rs = r < 49 ? r : 48;
+            glds16((const char*)dy + rs * 128 + 16 * (pc ^ c2_f(r)), slot_lds + c3::XB + (j - c3::NX) * 1024);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256, 1) void conv3_bwd_fr(const __bf16* __restrict__ a2,
+                                                       const __bf16* __restrict__ da3,
+                                                       const __bf16* __restrict__ w3d,  // [64 ci][576]
+                                                       __bf16* __restrict__ da2,
+                                                       float* __restrict__ slab,     // [grid][576][64]
+                                                       float* __restrict__ cs_slab,  // [grid][64]
+                                                       int nframes) {
+    __shared__ __attribute__((aligned(16))) char smem[c3::RING * c3::SLOT + c3::OUTT + c3::ZERO];
+    const int lane = threadIdx.x & 63;
+    const int w = wave_id();
+    const int g = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3, h = lane >> 5;
+    const uint32_t lds0 = lds_addr(smem);
+    __bf16* outt = (__bf16*)(smem + c3::RING * c3::SLOT);
+    char* zero = smem + c3::RING * c3::SLOT + c3::OUTT;
+    if (threadIdx.x < 16) ((uint32_t*)zero)[threadIdx.x] = 0u;
+
+    // dgrad B (16x16x32): lane holds W[k = 32ks + 8*(lane>>4) + j][ci = 16w + (lane&15)]
+    s16x8 bw[18];
+#pragma unroll
+    for (int ks = 0; ks < 18; ++ks)
+        bw[ks] = *(const s16x8*)(w3d + (size_t)(16 * w + (lane & 15)) * 576 + 32 * ks + 8 * g);
+
+    // ---- frame-invariant per-lane LDS offsets (relative to the slot base)
+    int wb_addr[4][2][2];  // wgrad B tr reads [ms][ct][lo/hi]
+#pragma unroll
+    for (int ms = 0; ms < 4; ++ms) {
+        const int mlo = ms * 16 + 8 * (g >> 1) + q, mhi = mlo + 4;
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {
+            const int c = 4 * ct + 2 * (g & 1) + (p4 >> 1);
+            wb_addr[ms][ct][0] = c3::XB + c2_dyaddr(mlo, c) + 8 * (p4 & 1);
+            wb_addr[ms][ct][1] = c3::XB + c2_dyaddr(mhi, c) + 8 * (p4 & 1);
+        }
+    }
+    const int mb3 = 48 + 8 * (g >> 1);  // last K-step: element j <-> m = mb3 + j
+    int wa_addr[5][4][2];  // wgrad A tr reads [i-th k-tile of this wave][ms][lo/hi]
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        const int kt = min(w + 4 * i, 17);
+        const int tap = kt >> 1, ky = tap / 3, kx = tap - 3 * ky;
+        const int ci = 32 * (kt & 1) + 16 * (g & 1) + 4 * p4;
+#pragma unroll
+        for (int ms = 0; ms < 4; ++ms) {
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+                const int m = min(ms * 16 + 8 * (g >> 1) + q + 4 * hh, 48);
+                const int oy = m / 7, ox = m - 7 * oy;
+                wa_addr[i][ms][hh] = c3_xaddr((oy + ky) * 9 + ox + kx, ci);
+            }
+        }
+    }
+    const int nkt = (18 - w + 3) / 4;  // k-tiles of this wave: 5,5,4,4
+    // dgrad A (16x16x32): row = input pixel rt*16 + (lane&15), k = 32ks + 8g -> tap ks>>1
+    uint32_t da_addr[6][9];  // [rt][tap] byte offset of the dY row (or the zero row) + chunk base
+#pragma unroll
+    for (int rt = 0; rt < 6; ++rt) {
+        const int pix = min(rt * 16 + (lane & 15), 80);
+        const int iy = pix / 9, ix = pix - 9 * iy;
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+            const int ky = tap / 3, kx = tap - 3 * ky;
+            const int oy = iy - ky, ox = ix - kx;
+            const bool ok = oy >= 0 && ox >= 0 && oy < 7 && ox < 7;
+            da_addr[rt][tap] = ok ? (uint32_t)((oy * 7 + ox) | 0x10000) : 0u;  // row | valid
+        }
+    }
+
+    f32x16 accw[5][2];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) { accw[i][0] = f32x16{}; accw[i][1] = f32x16{}; }
+    float bsum0 = 0.f, bsum1 = 0.f;
+
+    const int npw = (c3::NPIECE - w + 3) / 4;
+    constexpr int STORES = c3::OUT_CH / 256;  // 2 (waves 0..1 issue a third)
+    int issued = 0, m0 = 0, m1 = 0, m2 = 0;
+    const int nmine = nframes > (int)blockIdx.x ? (nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+    for (int i = 0; i < 3 && i < nmine; ++i) {
+        const int f = blockIdx.x + i * gridDim.x;
+        c3_issue(a2 + (size_t)f * 5184, da3 + (size_t)f * 3136, lds0 + i * c3::SLOT, w, lane);
+        issued += npw;
+        if (i == 0) m0 = issued; else if (i == 1) m1 = issued; else m2 = issued;
+    }
+    for (int it = 0; it < nmine; ++it) {
+        const int f = blockIdx.x + it * gridDim.x;
+        const int slot = it % 3;
+        char* X = smem + slot * c3::SLOT;
+        wait_vmcnt(issued - m0);
+        lds_barrier();
+
+        // ---------------- weight gradient (32x32x16, tr reads)
+#pragma unroll
+        for (int ms = 0; ms < 4; ++ms) {
+            bf16x8 bfr[2];
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct) {
+                bf16x8 v = tr2(X + wb_addr[ms][ct][0], X + wb_addr[ms][ct][1]);
+                if (ms == 3) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j)
+                        if (mb3 + j >= 49) v[j] = (__bf16)0.f;
+                }
+                bfr[ct] = v;
+                if (w == 0) {
+                    float sacc = 0.f;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) sacc += (float)v[j];
+                    if (ct == 0) bsum0 += sacc; else bsum1 += sacc;
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 5; ++i) {
+                if (i < nkt) {
+                    const bf16x8 afr = tr2(X + wa_addr[i][ms][0], X + wa_addr[i][ms][1]);
+                    accw[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, bfr[0], accw[i][0], 0, 0, 0);
+                    accw[i][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, bfr[1], accw[i][1], 0, 0, 0);
+                }
+            }
+        }
+
+        // ---------------- data gradient (16x16x32): channels 16w.., 6 row tiles
+#pragma unroll
+        for (int rt = 0; rt < 6; ++rt) {
+            f32x4 acc = {};
+#pragma unroll
+            for (int ks = 0; ks < 18; ++ks) {
+                const uint32_t e = da_addr[rt][ks >> 1];
+                const int row = e & 0xffff;
+                const int c = 4 * (ks & 1) + g;  // co chunk: co0 = 32*(ks&1) + 8g
+                const char* src = (e >> 16) ? X + c3::XB + c2_dyaddr(row, c) : zero;
+                const s16x8 a = *(const s16x8*)src;
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                             __builtin_bit_cast(bf16x8, bw[ks]), acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = rt * 16 + 4 * g + r;
+                outt[row * 64 + 16 * w + (lane & 15)] = (__bf16)acc[r];
+            }
+        }
+        lds_barrier();  // dgrad tile complete
+        {
+            u32x4* dst = (u32x4*)(da2 + (size_t)f * 5184);
+#pragma unroll
+            for (int i = 0; i < (c3::OUT_CH + 255) / 256; ++i) {
+                const int P = threadIdx.x + 256 * i;
+                if (P < c3::OUT_CH) {
+                    const int pix = P >> 3, c = P & 7;
+                    const bf16x8 v = *(const bf16x8*)(outt + pix * 64 + 8 * c);
+                    const bf16x8 m = *(const bf16x8*)(X + c3_xaddr(pix, 8 * c));
+                    bf16x8 o;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) o[j] = (float)m[j] > 0.f ? v[j] : (__bf16)0.f;
+                    __builtin_nontemporal_store(__builtin_bit_cast(u32x4, o), dst + P);
+                }
+            }
+            issued += STORES;
+        }
+        lds_barrier();  // slot fully consumed
+        int m3 = 0;
+        if (it + 3 < nmine) {
+            const int fn = blockIdx.x + (it + 3) * gridDim.x;
+            c3_issue(a2 + (size_t)fn * 5184, da3 + (size_t)fn * 3136, lds0 + slot * c3::SLOT, w, lane);
+            issued += npw;
+            m3 = issued;
+        }
+        m0 = m1;
+        m1 = m2;
+        m2 = m3;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    float* out = slab + (size_t)blockIdx.x * 576 * 64;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        if (i < nkt) {
+            const int kt = w + 4 * i;
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int k = 32 * kt + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    out[k * 64 + 32 * ct + (lane & 31)] = accw[i][ct][r];
+                }
+        }
+    }
+    if (w == 0) {
+        const float o0 = __shfl_xor(bsum0, 32, 64), o1 = __shfl_xor(bsum1, 32, 64);
+        if (lane < 32) {
+            cs_slab[(size_t)blockIdx.x * 64 + lane] = bsum0 + o0;
+            cs_slab[(size_t)blockIdx.x * 64 + 32 + lane] = bsum1 + o1;
+        }
+    }
+}
+
+int conv3_bwd_fr_launch(const __bf16* a2, const __bf16* da3, const __bf16* w3d, __bf16* da2,
+                        float* slab, float* cs_slab, int nframes, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(conv3_bwd_fr, dim3(grid), dim3(256), 0, s, a2, da3, w3d, da2, slab, cs_slab,
                        nframes);
     FI_HIP_CHECK(hipGetLastError());
     return FI_OK;

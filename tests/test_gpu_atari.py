@@ -136,6 +136,7 @@ def test_frame_resident_kernels_match_generic_path(monkeypatch):
         L.step_resident()
         N = (T + 1) * B
         outs[mode] = dict(a1=bf16_to_f32(L.tensor("a1", np.uint16, (N, 400 * 32))),
+                          da2=bf16_to_f32(L.tensor("da2", np.uint16, (N, 81 * 64))),
                           da1=bf16_to_f32(L.tensor("da1", np.uint16, (N, 400 * 32))),
                           g=L.tensor("grads"))
         L.close()
@@ -146,3 +147,6 @@ def test_frame_resident_kernels_match_generic_path(monkeypatch):
     rel(a["g"][8192:8224], b["g"][8192:8224], "c1b", l2=1e-4, mx=1e-3)
     rel(a["g"][8224:8224 + 32768], b["g"][8224:8224 + 32768], "c2W", l2=1e-4, mx=1e-3)
     rel(a["g"][40992:41056], b["g"][40992:41056], "c2b", l2=1e-4, mx=1e-3)
+    rel(a["da2"], b["da2"], "da2", l2=1e-3, mx=1e-2)
+    rel(a["g"][41056:41056 + 36864], b["g"][41056:41056 + 36864], "c3W", l2=1e-4, mx=1e-3)
+    rel(a["g"][77920:77984], b["g"][77920:77984], "c3b", l2=1e-4, mx=1e-3)
