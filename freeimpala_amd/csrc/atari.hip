@@ -530,10 +530,10 @@ int conv1_fwd_fr_launch(const uint8_t* frames, const __bf16* w1t, const float* b
                         int nframes, int grid, hipStream_t s);
 int conv1_wgrad_fr_launch(const uint8_t* frames, const __bf16* da1, float* slab, float* cs_slab,
                           int nframes, int grid, hipStream_t s);
-int conv2_bwd_fr_launch(const __bf16* a1, const __bf16* da2, const __bf16* w2d, __bf16* da1,
-                        float* slab, float* cs_slab, int nframes, int grid, hipStream_t s);
-int conv3_bwd_fr_launch(const __bf16* a2, const __bf16* da3, const __bf16* w3d, __bf16* da2,
-                        float* slab, float* cs_slab, int nframes, int grid, hipStream_t s);
+int conv2_bwd_fr_launch(const __bf16* a1, const __bf16* da2, const __bf16* w2d, __bf16* da1, float* slab,
+                        float* cs_slab, int nframes, int grid, hipStream_t s);
+int conv3_bwd_fr_launch(const __bf16* a2, const __bf16* da3, const __bf16* w3d, __bf16* da2, float* slab,
+                        float* cs_slab, int nframes, int grid, hipStream_t s);
 constexpr int FR_GRID = 256;  // persistent frame-resident workgroups (1 per CU)
 
 static AtariImpl* impl(AtariNet* n) { return (AtariImpl*)n->impl; }

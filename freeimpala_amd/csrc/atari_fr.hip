@@ -248,56 +248,60 @@ int conv1_wgrad_fr_launch(const uint8_t* frames, const __bf16* da1, float* slab,
 
 
 // =====================================================================================
-// conv2 backward, fused and frame-resident (4x4 / stride 2, 32 -> 64 channels, 20x20 -> 9x9)
-//   in : X = a1[f] (20,20,32) bf16 (layer input = ReLU mask),  dY = da2[f] (9,9,64) bf16
-//   out: da1[f] = (X > 0) * dgrad(dY, W2)   (written in place over X in LDS, then stored)
-//        dW2 += im2col(X)^T dY  (512 x 64, registers across frames),  db2 += sum dY
-// LDS ring of 3 frames, filled by LDS-DMA (global_load_lds_dwordx4), counted vmcnt.
-//   X image : pixel p at 256*(p>>2) + 64*sigma(p), sigma(p) = ((p&3) + ((p>>2)&1)) & 3
-//             -> the four stride-2 pixels a transposed read gathers sit in different
-//                quarters of a 256-byte bank row (conflict-free ds_read_b64_tr_b16)
-//   dY tile : row r (output pixel) at 128*r, 16-byte chunk c at 16*(c ^ f(r)),
-//             f(r) = (((r>>1)&1)<<2) | ((r>>2)&3): conflict-free both for the b128 row
-//             reads of the dgrad and the transposed reads of the wgrad.
-// wgrad: wave w owns taps (ky=w, kx=0..3) = k rows [128w, 128w+128) x 64 co.
-// dgrad: wave w owns parity class (py, px) = (w>>1, w&1): 100 input pixels (4 row tiles),
-//        K = (ty, tx, co) = 256, W2 class slice kept in registers (64 VGPRs).
+// Fused, frame-resident conv backward kernels (dgrad + wgrad + bias of one layer).
+// Per frame, LDS holds the layer input X (= ReLU mask of the data gradient) and the
+// upstream gradient dY; the kernel writes dX = (X > 0) * dgrad(dY, W) once and keeps
+// dW / db accumulating in registers across its frames (one fp32 partial slab per
+// workgroup, reduced in a fixed order afterwards). Frames stream through a 3-deep LDS ring
+// filled by LDS-DMA (global_load_lds_dwordx4) with counted vmcnt waits.
+//
+// Layouts are chosen so that every MFMA fragment address is a per-lane base register plus
+// a compile-time immediate (no per-K-step address arithmetic, registers left for the
+// compiler to keep several LDS reads in flight):
+//   X  : linear NHWC, 2*C bytes per pixel.
+//   dY : zero-bordered (OH + 2*pad)^2 pixel rows, pitch 144 B (8 data + 1 pad slot): the
+//        dgrad gather reads row (base - tap) with no bounds checks, and 16 consecutive
+//        rows hit 16 distinct 16-byte slots (9 is odd) -> conflict-free ds_read_b128.
+//        Border and pad slots are DMA'd from a 16-byte zero buffer in global memory.
+// wgrad: A^T = im2col(X) and B = dY are read with ds_read_b64_tr_b16 (transposed MFMA
+//        operands, reduction over the output pixels).
 // =====================================================================================
+constexpr int DP = 144;  // padded dY pitch (bytes)
+
+__device__ __forceinline__ uint32_t dy_piece_off(int P, int npix_side, int pad) {
+    // physical 16-byte piece P of the zero-bordered dY tile -> byte offset in the frame's
+    // dY (FI_OOB for border / pad slots: the buffer range check returns zeros)
+    const int side = npix_side + 2 * pad;
+    const int R = P / 9, c = P - 9 * R;
+    const int ry = R / side, rx = R - side * ry;
+    const bool inside = R < side * side && c < 8 && ry >= pad && rx >= pad && ry < pad + npix_side &&
+                        rx < pad + npix_side;
+    return inside ? (uint32_t)(((ry - pad) * npix_side + (rx - pad)) * 128 + 16 * c) : FI_OOB;
+}
+
 namespace c2 {
-constexpr int XB = 20 * 20 * 32 * 2;         // 25,600
-constexpr int DYROWS = 96;                   // 81 rows padded to 6 MFMA K-steps
-constexpr int DYB = DYROWS * 128;            // 12,288
-constexpr int SLOT = XB + DYB;               // 37,888
+constexpr int XB = 20 * 20 * 64;             // 25,600: a1 tile, linear NHWC
+constexpr int DYB = 18 * 1024;               // 11x11 bordered rows * 144 B = 17,424 -> 18 KiB
+constexpr int SLOT = XB + DYB;               // 44,032
 constexpr int RING = 3;
-constexpr int NX = XB / 1024;                // 25 LDS-DMA pieces (1 KiB each)
-constexpr int NDY = DYB / 1024;              // 12
-constexpr int NPIECE = NX + NDY;             // 37
-constexpr int OUT_CH = XB / 16;              // 1600 16-byte chunks of da1
-constexpr int OUTT = 4 * 128 * 32 * 2;       // 32 KiB dgrad tile in accumulator order
+constexpr int NX = XB / 1024, NDY = 18;  // 25 + 18 pieces
+constexpr int OUTT = 4 * 100 * 64;           // dgrad tile [class][100][32 ci] bf16
+constexpr int OUT_CH = XB / 16;              // 1600
 }  // namespace c2
 
-__device__ __forceinline__ int c2_sigma(int p) { return ((p & 3) + ((p >> 2) & 1)) & 3; }
-__device__ __forceinline__ int c2_xaddr(int p) { return 256 * (p >> 2) + 64 * c2_sigma(p); }
-__device__ __forceinline__ int c2_f(int r) { return (((r >> 1) & 1) << 2) | ((r >> 2) & 3); }
-__device__ __forceinline__ int c2_dyaddr(int r, int c) { return 128 * r + 16 * (c ^ c2_f(r)); }
-
-__device__ __forceinline__ void c2_issue(const __bf16* x, const __bf16* dy, uint32_t slot_lds,
-                                         int w, int lane) {
+// wave w DMAs X pieces j = w + 4i (< 25) and dY pieces d = w + 4k (< 18)
+__device__ __forceinline__ void c2_issue(const __bf16* x, const __bf16* dy, const uint32_t (&dvo)[5],
+                                         uint32_t slot_lds, int w, int lane) {
+    const fi_i32x4 xr = make_rsrc(x, 25600), dr = make_rsrc(dy, 10368);
 #pragma unroll
-    for (int i = 0; i < (c2::NPIECE + 3) / 4; ++i) {
+    for (int i = 0; i < 7; ++i) {
         const int j = w + 4 * i;
-        if (j >= c2::NPIECE) break;
-        if (j < c2::NX) {
-            const int P = j * 64 + lane;  // physical 16-byte piece of the X image
-            const int G = P >> 4, s = (P >> 2) & 3, c = P & 3;
-            const int p = 4 * G + ((s - (G & 1)) & 3);
-            glds16((const char*)x + p * 64 + c * 16, slot_lds + j * 1024);
-        } else {
-            const int P = (j - c2::NX) * 64 + lane;  // physical piece of the dY tile
-            const int r = P >> 3, pc = P & 7;
-            const int rs = r < 81 ? r : 80;
-            glds16((const char*)dy + rs * 128 + 16 * (pc ^ c2_f(r)), slot_lds + c2::XB + (j - c2::NX) * 1024);
-        }
+        if (i < 6 || j < c2::NX) blds16(xr, 16 * lane + 1024 * j, slot_lds + j * 1024);
+    }
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const int d = w + 4 * k;
+        if (k < 4 || d < c2::NDY) blds16(dr, dvo[k], slot_lds + c2::XB + d * 1024);
     }
 }
 
@@ -305,73 +309,55 @@ __global__ __launch_bounds__(256, 1) void conv2_bwd_fr(const __bf16* __restrict_
                                                        const __bf16* __restrict__ da2,
                                                        const __bf16* __restrict__ w2d,  // [4][32][256]
                                                        __bf16* __restrict__ da1,
-                                                       float* __restrict__ slab,   // [grid][512][64]
+                                                       float* __restrict__ slab,     // [grid][512][64]
                                                        float* __restrict__ cs_slab,  // [grid][64]
                                                        int nframes) {
     __shared__ __attribute__((aligned(16))) char smem[c2::RING * c2::SLOT + c2::OUTT];
     const int lane = threadIdx.x & 63;
     const int w = wave_id();
     const int g = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3, h = lane >> 5, col = lane & 31;
-    __bf16* outt = (__bf16*)(smem + c2::RING * c2::SLOT);  // [cls][128][32], unmasked dX
     const uint32_t lds0 = lds_addr(smem);
+    __bf16* outt = (__bf16*)(smem + c2::RING * c2::SLOT);
 
     // dgrad B fragments (class w): W[k = 16ks + 8h + j][ci = col]
     bf16x8 bw[16];
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks) bw[ks] = *(const bf16x8*)(w2d + ((size_t)(w * 32 + col)) * 256 + ks * 16 + h * 8);
+
+    // ---- per-lane base offsets (relative to a ring slot); everything else is immediate
+    int ba[6][2], bb[6][2];  // wgrad A (X, tap ky = w, kx = 0 -> +64*kx) / wgrad B (dY, ct -> +64)
+#pragma unroll
+    for (int ms = 0; ms < 6; ++ms)
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            const int mu = ms * 16 + 8 * (g >> 1) + q + 4 * hh;
+            const int m = min(mu, 80), oy = m / 9, ox = m - 9 * oy;
+            ba[ms][hh] = 64 * ((2 * oy + w) * 20 + 2 * ox) + 2 * (16 * (g & 1) + 4 * p4);
+            const int mb = min(mu, 89), by = mb / 9, bx = mb - 9 * by;  // m >= 81 -> zero border
+            bb[ms][hh] = c2::XB + DP * ((by + 1) * 11 + bx + 1) + 2 * (16 * (g & 1) + 4 * p4);
+        }
+    uint32_t dvo[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) dvo[k] = dy_piece_off(64 * (w + 4 * k) + lane, 9, 1);
+    int bd[4];  // dgrad A: dY row of (iyq - ty, ixq - tx) = base - 144*(11 ty + tx)
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt) {
+        const int r = min(rt * 32 + col, 99), iyq = r / 10, ixq = r - 10 * iyq;
+        bd[rt] = c2::XB + DP * ((iyq + 1) * 11 + ixq + 1 - 12) + 16 * h;
+    }
+
     f32x16 accw[4][2];
 #pragma unroll
     for (int t = 0; t < 4; ++t) { accw[t][0] = f32x16{}; accw[t][1] = f32x16{}; }
     float bsum0 = 0.f, bsum1 = 0.f;
 
-    // ---- frame-invariant LDS addresses (byte offsets inside a ring slot), per lane
-    // wgrad B (dY, tr reads): [ms][ct][lo/hi]
-    int wb_addr[6][2][2];
-    // wgrad A (X image, tr reads): [ms][tap kx][lo/hi]
-    int wa_addr[6][4][2];
-#pragma unroll
-    for (int ms = 0; ms < 6; ++ms) {
-        const int mlo = ms * 16 + 8 * (g >> 1) + q, mhi = mlo + 4;
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct) {
-            const int c = 4 * ct + 2 * (g & 1) + (p4 >> 1);
-            wb_addr[ms][ct][0] = c2::XB + c2_dyaddr(mlo, c) + 8 * (p4 & 1);
-            wb_addr[ms][ct][1] = c2::XB + c2_dyaddr(mhi, c) + 8 * (p4 & 1);
-        }
-        const int ml = min(mlo, 80), mh = min(mhi, 80);
-        const int oyl = ml / 9, oxl = ml - oyl * 9, oyh = mh / 9, oxh = mh - oyh * 9;
-        const int ci = 16 * (g & 1) + 4 * p4;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            wa_addr[ms][t][0] = c2_xaddr((2 * oyl + w) * 20 + 2 * oxl + t) + 2 * ci;
-            wa_addr[ms][t][1] = c2_xaddr((2 * oyh + w) * 20 + 2 * oxh + t) + 2 * ci;
-        }
-    }
-    // lanes whose B rows m = 80 + 8*(g>>1) + j pass 81 in the last K-step get zeroed there
-    const int mb5 = 80 + 8 * (g >> 1);
-    // dgrad A (dY rows, b128): [rt][ks] address and validity bit
-    int da_addr[4][16];
-    uint64_t da_ok = 0;
-#pragma unroll
-    for (int rt = 0; rt < 4; ++rt) {
-        const int r = min(rt * 32 + col, 99);
-        const int iyq = r / 10, ixq = r - iyq * 10;
-#pragma unroll
-        for (int ks = 0; ks < 16; ++ks) {
-            const int tap = ks >> 2, ty = tap >> 1, tx = tap & 1;
-            const int oy = iyq - ty, ox = ixq - tx;
-            const bool ok = oy >= 0 && ox >= 0 && oy < 9 && ox < 9;
-            da_addr[rt][ks] = c2::XB + c2_dyaddr(ok ? oy * 9 + ox : 0, 2 * (ks & 3) + h);
-            if (ok) da_ok |= 1ull << (rt * 16 + ks);
-        }
-    }
-    const int npw = (c2::NPIECE - w + 3) / 4;  // LDS-DMA pieces per wave per frame
-    constexpr int STORES = c2::OUT_CH / 256;   // 6 store instructions every wave surely issues
+    const int npw = (c2::NX - w + 3) / 4 + (c2::NDY - w + 3) / 4;
+    constexpr int STORES = c2::OUT_CH / 256;   // 6 store instructions every wave issues
     int issued = 0, m0 = 0, m1 = 0, m2 = 0;
     const int nmine = nframes > (int)blockIdx.x ? (nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
     for (int i = 0; i < 3 && i < nmine; ++i) {
         const int f = blockIdx.x + i * gridDim.x;
-        c2_issue(a1 + (size_t)f * 12800, da2 + (size_t)f * 5184, lds0 + i * c2::SLOT, w, lane);
+        c2_issue(a1 + (size_t)f * 12800, da2 + (size_t)f * 5184, dvo, lds0 + i * c2::SLOT, w, lane);
         issued += npw;
         if (i == 0) m0 = issued; else if (i == 1) m1 = issued; else m2 = issued;
     }
@@ -382,52 +368,50 @@ __global__ __launch_bounds__(256, 1) void conv2_bwd_fr(const __bf16* __restrict_
         wait_vmcnt(issued - m0);
         lds_barrier();
 
-        // ---------------- weight gradient: A^T = im2col(X) (tr reads), B = dY (tr reads)
+        // ---------------- weight gradient (taps ky = w, kx = 0..3)
 #pragma unroll
         for (int ms = 0; ms < 6; ++ms) {
-            bf16x8 bfr[2];
+            const bf16x8 b0 = tr2(X + bb[ms][0], X + bb[ms][1]);
+            const bf16x8 b1 = tr2(X + bb[ms][0] + 64, X + bb[ms][1] + 64);
+            if (w == 0) {
+                float s0 = 0.f, s1 = 0.f;
 #pragma unroll
-            for (int ct = 0; ct < 2; ++ct) {
-                bf16x8 v = tr2(X + wb_addr[ms][ct][0], X + wb_addr[ms][ct][1]);
-                if (ms == 5) {
-#pragma unroll
-                    for (int j = 0; j < 8; ++j)
-                        if (mb5 + j >= 81) v[j] = (__bf16)0.f;
-                }
-                bfr[ct] = v;
-                if (w == 0) {
-                    float sacc = 0.f;
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) sacc += (float)v[j];
-                    if (ct == 0) bsum0 += sacc; else bsum1 += sacc;
-                }
+                for (int j = 0; j < 8; ++j) { s0 += (float)b0[j]; s1 += (float)b1[j]; }
+                bsum0 += s0;
+                bsum1 += s1;
             }
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
-                const bf16x8 afr = tr2(X + wa_addr[ms][t][0], X + wa_addr[ms][t][1]);
-                accw[t][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, bfr[0], accw[t][0], 0, 0, 0);
-                accw[t][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, bfr[1], accw[t][1], 0, 0, 0);
+                const bf16x8 afr = tr2(X + ba[ms][0] + 64 * t, X + ba[ms][1] + 64 * t);
+                accw[t][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, b0, accw[t][0], 0, 0, 0);
+                accw[t][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, b1, accw[t][1], 0, 0, 0);
             }
         }
 
-        // ---------------- data gradient of class (py, px): rows = 100 input pixels
+        // ---------------- data gradient, parity class (w>>1, w&1); two row tiles in flight
 #pragma unroll
-        for (int rt = 0; rt < 4; ++rt) {
-            f32x16 acc = {};
+        for (int rp = 0; rp < 2; ++rp) {
+            f32x16 acc0 = {}, acc1 = {};
+            const char* base0 = X + bd[2 * rp];
+            const char* base1 = X + bd[2 * rp + 1];
 #pragma unroll
             for (int ks = 0; ks < 16; ++ks) {
-                bf16x8 a = *(const bf16x8*)(X + da_addr[rt][ks]);
-                if (!((da_ok >> (rt * 16 + ks)) & 1)) a = bf16x8{};
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bw[ks], acc, 0, 0, 0);
+                const int tap = ks >> 2, ty = tap >> 1, tx = tap & 1;
+                const int off = DP * (12 - (11 * ty + tx)) + 32 * (ks & 3);
+                const bf16x8 a0 = *(const bf16x8*)(base0 + off);
+                const bf16x8 a1 = *(const bf16x8*)(base1 + off);
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bw[ks], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bw[ks], acc1, 0, 0, 0);
             }
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int ri = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                outt[(w * 128 + ri) * 32 + col] = (__bf16)acc[r];
+                const int ri = rp * 64 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                outt[(w * 100 + ri) * 32 + col] = (__bf16)acc0[r];
+                if (ri + 32 < 100) outt[(w * 100 + ri + 32) * 32 + col] = (__bf16)acc1[r];
             }
         }
         lds_barrier();  // dgrad tile complete
-        {  // da1 = (X > 0) * dX, in NHWC order: chunk P = pixel P/4, channels 8*(P%4)..+8
+        {  // da1 = (X > 0) * dX in NHWC order: chunk P = pixel P/4, channels 8*(P%4)..+8
             u32x4* dst = (u32x4*)(da1 + (size_t)f * 12800);
 #pragma unroll
             for (int i = 0; i < (c2::OUT_CH + 255) / 256; ++i) {
@@ -436,8 +420,8 @@ __global__ __launch_bounds__(256, 1) void conv2_bwd_fr(const __bf16* __restrict_
                     const int pix = P >> 2, c = P & 3;
                     const int iy = pix / 20, ix = pix - iy * 20;
                     const int cls = ((iy & 1) << 1) | (ix & 1), ri = (iy >> 1) * 10 + (ix >> 1);
-                    const bf16x8 v = *(const bf16x8*)(outt + (cls * 128 + ri) * 32 + 8 * c);
-                    const bf16x8 m = *(const bf16x8*)(X + c2_xaddr(pix) + 16 * c);
+                    const bf16x8 v = *(const bf16x8*)(outt + (cls * 100 + ri) * 32 + 8 * c);
+                    const bf16x8 m = *(const bf16x8*)(X + 16 * P);
                     bf16x8 o;
 #pragma unroll
                     for (int j = 0; j < 8; ++j) o[j] = (float)m[j] > 0.f ? v[j] : (__bf16)0.f;
@@ -450,7 +434,7 @@ __global__ __launch_bounds__(256, 1) void conv2_bwd_fr(const __bf16* __restrict_
         int m3 = 0;
         if (it + 3 < nmine) {
             const int fn = blockIdx.x + (it + 3) * gridDim.x;
-            c2_issue(a1 + (size_t)fn * 12800, da2 + (size_t)fn * 5184, lds0 + slot * c2::SLOT, w, lane);
+            c2_issue(a1 + (size_t)fn * 12800, da2 + (size_t)fn * 5184, dvo, lds0 + slot * c2::SLOT, w, lane);
             issued += npw;
             m3 = issued;
         }
@@ -459,7 +443,6 @@ __global__ __launch_bounds__(256, 1) void conv2_bwd_fr(const __bf16* __restrict_
         m2 = m3;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    // weight-gradient partial: k = 128w + 32t + row, co = 32ct + col
     float* out = slab + (size_t)blockIdx.x * 512 * 64;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -470,8 +453,7 @@ __global__ __launch_bounds__(256, 1) void conv2_bwd_fr(const __bf16* __restrict_
                 const int k = 128 * w + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
                 out[k * 64 + 32 * ct + col] = accw[t][ct][r];
             }
-    // bias: wave 0 lanes l and l+32 hold the same co (16*(g&1) + (l&15)), different m halves
-    if (w == 0) {
+    if (w == 0) {  // lanes l and l+32 hold the same co (16*(g&1) + (l&15)), other m half
         const float o0 = __shfl_xor(bsum0, 32, 64), o1 = __shfl_xor(bsum1, 32, 64);
         if (lane < 32) {
             cs_slab[(size_t)blockIdx.x * 64 + lane] = bsum0 + o0;
@@ -480,62 +462,47 @@ __global__ __launch_bounds__(256, 1) void conv2_bwd_fr(const __bf16* __restrict_
     }
 }
 
-int conv2_bwd_fr_launch(const __bf16* a1, const __bf16* da2, const __bf16* w2d, __bf16* da1,
-                        float* slab, float* cs_slab, int nframes, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(conv2_bwd_fr, dim3(grid), dim3(256), 0, s, a1, da2, w2d, da1, slab, cs_slab,
-                       nframes);
+int conv2_bwd_fr_launch(const __bf16* a1, const __bf16* da2, const __bf16* w2d, __bf16* da1, float* slab,
+                        float* cs_slab, int nframes, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(conv2_bwd_fr, dim3(grid), dim3(256), 0, s, a1, da2, w2d, da1,
+                       slab, cs_slab, nframes);
     FI_HIP_CHECK(hipGetLastError());
     return FI_OK;
 }
 
-
-// =====================================================================================
-// conv3 backward, fused and frame-resident (3x3 / stride 1, 64 -> 64 channels, 9x9 -> 7x7)
-//   in : X = a2[f] (9,9,64), dY = da3[f] (7,7,64);  out: da2[f] = (X>0) * dgrad(dY, W3),
-//        dW3 (576 x 64) and db3 accumulated in registers across frames.
-// X image : pixel p at 128p, its 64-byte channel halves swapped when (p>>1)&1 -> the four
-//           consecutive pixels of a transposed read land in distinct bank quarters.
-// dY tile : 64 rows (49 valid) x 128 B, chunk swizzle c ^ f(r) as in conv2.
-// wgrad: 32x32x16 MFMA, k-tile kt = (tap, 32-channel half), waves take kt = w, w+4, ...
-// dgrad: 16x16x32 MFMA, wave w owns input channels 16w..16w+15 for all 6 row tiles of 16
-//        input pixels; its W3 slice (18 K-steps) lives in registers; taps that fall
-//        outside the 7x7 output read a 16-byte zero row instead of being masked.
-// =====================================================================================
+// ------------------------------------------------------------------------------------
+// conv3 backward (3x3 / stride 1, 9x9x64 -> 7x7x64). dgrad on 16x16x32 MFMAs: wave w owns
+// input channels 16w..16w+15 for all 6 row tiles of 16 input pixels (W3 slice of 18
+// K-steps in registers); wgrad on 32x32x16: k-tile kt = w + 4i = (tap 2i + (w>>1),
+// channel half w&1).
+// ------------------------------------------------------------------------------------
 namespace c3 {
 constexpr int XB = 11 * 1024;                // 81 px * 128 B = 10,368, padded to 11 KiB
-constexpr int DYB = 64 * 128;                // 8 KiB
-constexpr int SLOT = XB + DYB;               // 19,456
+constexpr int DYB = 18 * 1024;               // 11x11 bordered rows * 144 B = 17,424
+constexpr int SLOT = XB + DYB;               // 29,696
 constexpr int RING = 3;
-constexpr int NX = 11, NDY = 8, NPIECE = NX + NDY;   // 19 LDS-DMA pieces
-constexpr int OUTT = 96 * 128;               // dgrad tile [96 rows][64 ci] bf16
-constexpr int ZERO = 64;                     // zero row (16 B used)
-constexpr int OUT_CH = 81 * 8;               // 648 16-byte chunks of da2
+constexpr int NX = 11, NDY = 18;  // 11 + 18 pieces
+constexpr int OUTT = 81 * 128;               // dgrad tile [81][64] bf16
+constexpr int OUT_CH = 81 * 8;               // 648
 }  // namespace c3
 
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ int c3_xaddr(int p, int ci) {  // byte offset of (pixel, channel)
-    return 128 * p + 64 * ((ci >> 5) ^ ((p >> 1) & 1)) + 2 * (ci & 31);
-}
-
-__device__ __forceinline__ void c3_issue(const __bf16* x, const __bf16* dy, uint32_t slot_lds,
-                                         int w, int lane) {
+// wave w DMAs X pieces j = w + 4i (< 11; lanes past pixel 81 read zeros) and dY pieces
+// d = w + 4k (< 18)
+__device__ __forceinline__ void c3_issue(const __bf16* x, const __bf16* dy, const uint32_t (&dvo)[5],
+                                         uint32_t slot_lds, int w, int lane) {
+    const fi_i32x4 xr = make_rsrc(x, 10368), dr = make_rsrc(dy, 6272);
 #pragma unroll
-    for (int i = 0; i < (c3::NPIECE + 3) / 4; ++i) {
+    for (int i = 0; i < 3; ++i) {
         const int j = w + 4 * i;
-        if (j >= c3::NPIECE) break;
-        if (j < c3::NX) {
-            const int P = j * 64 + lane;         // physical 16-byte piece of the X image
-            const int p = min(P >> 3, 80), pc = P & 7;
-            const int lc = 4 * ((pc >> 2) ^ ((p >> 1) & 1)) + (pc & 3);  // logical chunk
-            glds16((const char*)x + p * 128 + 16 * lc, slot_lds + j * 1024);
-        } else {
-            const int P = (j - c3::NX) * 64 + lane;
-            const int r = P >> 3, pc = P & 7;
-            const int rs = r < 49 ? r : 48;
-            glds16((const char*)dy + rs * 128 + 16 * (pc ^ c2_f(r)), slot_lds + c3::XB + (j - c3::NX) * 1024);
-        }
+        if (i < 2 || j < c3::NX) blds16(xr, 16 * lane + 1024 * j, slot_lds + j * 1024);
+    }
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const int d = w + 4 * k;
+        if (k < 4 || d < c3::NDY) blds16(dr, dvo[k], slot_lds + c3::XB + d * 1024);
     }
 }
 
@@ -546,64 +513,46 @@ __global__ __launch_bounds__(256, 1) void conv3_bwd_fr(const __bf16* __restrict_
                                                        float* __restrict__ slab,     // [grid][576][64]
                                                        float* __restrict__ cs_slab,  // [grid][64]
                                                        int nframes) {
-    __shared__ __attribute__((aligned(16))) char smem[c3::RING * c3::SLOT + c3::OUTT + c3::ZERO];
+    __shared__ __attribute__((aligned(16))) char smem[c3::RING * c3::SLOT + c3::OUTT];
     const int lane = threadIdx.x & 63;
     const int w = wave_id();
     const int g = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3, h = lane >> 5;
     const uint32_t lds0 = lds_addr(smem);
     __bf16* outt = (__bf16*)(smem + c3::RING * c3::SLOT);
-    char* zero = smem + c3::RING * c3::SLOT + c3::OUTT;
-    if (threadIdx.x < 16) ((uint32_t*)zero)[threadIdx.x] = 0u;
 
-    // dgrad B (16x16x32): lane holds W[k = 32ks + 8*(lane>>4) + j][ci = 16w + (lane&15)]
+    // dgrad B (16x16x32): lane holds W[k = 32ks + 8g + j][ci = 16w + (lane&15)]
     s16x8 bw[18];
 #pragma unroll
     for (int ks = 0; ks < 18; ++ks)
         bw[ks] = *(const s16x8*)(w3d + (size_t)(16 * w + (lane & 15)) * 576 + 32 * ks + 8 * g);
 
-    // ---- frame-invariant per-lane LDS offsets (relative to the slot base)
-    int wb_addr[4][2][2];  // wgrad B tr reads [ms][ct][lo/hi]
-#pragma unroll
-    for (int ms = 0; ms < 4; ++ms) {
-        const int mlo = ms * 16 + 8 * (g >> 1) + q, mhi = mlo + 4;
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct) {
-            const int c = 4 * ct + 2 * (g & 1) + (p4 >> 1);
-            wb_addr[ms][ct][0] = c3::XB + c2_dyaddr(mlo, c) + 8 * (p4 & 1);
-            wb_addr[ms][ct][1] = c3::XB + c2_dyaddr(mhi, c) + 8 * (p4 & 1);
-        }
-    }
-    const int mb3 = 48 + 8 * (g >> 1);  // last K-step: element j <-> m = mb3 + j
-    int wa_addr[5][4][2];  // wgrad A tr reads [i-th k-tile of this wave][ms][lo/hi]
+    // wgrad tap offsets of this wave's k-tiles (wave-uniform): tap = 2i + (w>>1)
+    int toff[5];
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
-        const int kt = min(w + 4 * i, 17);
-        const int tap = kt >> 1, ky = tap / 3, kx = tap - 3 * ky;
-        const int ci = 32 * (kt & 1) + 16 * (g & 1) + 4 * p4;
-#pragma unroll
-        for (int ms = 0; ms < 4; ++ms) {
-#pragma unroll
-            for (int hh = 0; hh < 2; ++hh) {
-                const int m = min(ms * 16 + 8 * (g >> 1) + q + 4 * hh, 48);
-                const int oy = m / 7, ox = m - 7 * oy;
-                wa_addr[i][ms][hh] = c3_xaddr((oy + ky) * 9 + ox + kx, ci);
-            }
-        }
+        const int t = min(2 * i + (w >> 1), 8), ky = t / 3, kx = t - 3 * ky;
+        toff[i] = __builtin_amdgcn_readfirstlane(128 * (9 * ky + kx));
     }
-    const int nkt = (18 - w + 3) / 4;  // k-tiles of this wave: 5,5,4,4
-    // dgrad A (16x16x32): row = input pixel rt*16 + (lane&15), k = 32ks + 8g -> tap ks>>1
-    uint32_t da_addr[6][9];  // [rt][tap] byte offset of the dY row (or the zero row) + chunk base
+    const int nkt = (18 - w + 3) / 4;  // 5,5,4,4
+    int ba[4][2], bb[4][2];
+#pragma unroll
+    for (int ms = 0; ms < 4; ++ms)
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            const int mu = ms * 16 + 8 * (g >> 1) + q + 4 * hh;
+            const int m = min(mu, 48), oy = m / 7, ox = m - 7 * oy;
+            ba[ms][hh] = 128 * (oy * 9 + ox) + 2 * (32 * (w & 1) + 16 * (g & 1) + 4 * p4);
+            const int mb = min(mu, 55), by = mb / 7, bx = mb - 7 * by;  // m >= 49 -> zero border
+            bb[ms][hh] = c3::XB + DP * ((by + 2) * 11 + bx + 2) + 2 * (16 * (g & 1) + 4 * p4);
+        }
+    uint32_t dvo[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) dvo[k] = dy_piece_off(64 * (w + 4 * k) + lane, 7, 2);
+    int bd[6];
 #pragma unroll
     for (int rt = 0; rt < 6; ++rt) {
-        const int pix = min(rt * 16 + (lane & 15), 80);
-        const int iy = pix / 9, ix = pix - 9 * iy;
-#pragma unroll
-        for (int tap = 0; tap < 9; ++tap) {
-            const int ky = tap / 3, kx = tap - 3 * ky;
-            const int oy = iy - ky, ox = ix - kx;
-            const bool ok = oy >= 0 && ox >= 0 && oy < 7 && ox < 7;
-            da_addr[rt][tap] = ok ? (uint32_t)((oy * 7 + ox) | 0x10000) : 0u;  // row | valid
-        }
+        const int pix = min(rt * 16 + (lane & 15), 80), iy = pix / 9, ix = pix - 9 * iy;
+        bd[rt] = c3::XB + DP * ((iy + 2) * 11 + ix + 2 - 24) + 16 * g;
     }
 
     f32x16 accw[5][2];
@@ -611,13 +560,13 @@ __global__ __launch_bounds__(256, 1) void conv3_bwd_fr(const __bf16* __restrict_
     for (int i = 0; i < 5; ++i) { accw[i][0] = f32x16{}; accw[i][1] = f32x16{}; }
     float bsum0 = 0.f, bsum1 = 0.f;
 
-    const int npw = (c3::NPIECE - w + 3) / 4;
-    constexpr int STORES = c3::OUT_CH / 256;  // 2 (waves 0..1 issue a third)
+    const int npw = (c3::NX - w + 3) / 4 + (c3::NDY - w + 3) / 4;
+    constexpr int STORES = c3::OUT_CH / 256;  // 2
     int issued = 0, m0 = 0, m1 = 0, m2 = 0;
     const int nmine = nframes > (int)blockIdx.x ? (nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
     for (int i = 0; i < 3 && i < nmine; ++i) {
         const int f = blockIdx.x + i * gridDim.x;
-        c3_issue(a2 + (size_t)f * 5184, da3 + (size_t)f * 3136, lds0 + i * c3::SLOT, w, lane);
+        c3_issue(a2 + (size_t)f * 5184, da3 + (size_t)f * 3136, dvo, lds0 + i * c3::SLOT, w, lane);
         issued += npw;
         if (i == 0) m0 = issued; else if (i == 1) m1 = issued; else m2 = issued;
     }
@@ -628,54 +577,50 @@ __global__ __launch_bounds__(256, 1) void conv3_bwd_fr(const __bf16* __restrict_
         wait_vmcnt(issued - m0);
         lds_barrier();
 
-        // ---------------- weight gradient (32x32x16, tr reads)
+        // ---------------- weight gradient
 #pragma unroll
         for (int ms = 0; ms < 4; ++ms) {
-            bf16x8 bfr[2];
+            const bf16x8 b0 = tr2(X + bb[ms][0], X + bb[ms][1]);
+            const bf16x8 b1 = tr2(X + bb[ms][0] + 64, X + bb[ms][1] + 64);
+            if (w == 0) {
+                float s0 = 0.f, s1 = 0.f;
 #pragma unroll
-            for (int ct = 0; ct < 2; ++ct) {
-                bf16x8 v = tr2(X + wb_addr[ms][ct][0], X + wb_addr[ms][ct][1]);
-                if (ms == 3) {
-#pragma unroll
-                    for (int j = 0; j < 8; ++j)
-                        if (mb3 + j >= 49) v[j] = (__bf16)0.f;
-                }
-                bfr[ct] = v;
-                if (w == 0) {
-                    float sacc = 0.f;
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) sacc += (float)v[j];
-                    if (ct == 0) bsum0 += sacc; else bsum1 += sacc;
-                }
+                for (int j = 0; j < 8; ++j) { s0 += (float)b0[j]; s1 += (float)b1[j]; }
+                bsum0 += s0;
+                bsum1 += s1;
             }
 #pragma unroll
             for (int i = 0; i < 5; ++i) {
                 if (i < nkt) {
-                    const bf16x8 afr = tr2(X + wa_addr[i][ms][0], X + wa_addr[i][ms][1]);
-                    accw[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, bfr[0], accw[i][0], 0, 0, 0);
-                    accw[i][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, bfr[1], accw[i][1], 0, 0, 0);
+                    const bf16x8 afr = tr2(X + ba[ms][0] + toff[i], X + ba[ms][1] + toff[i]);
+                    accw[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, b0, accw[i][0], 0, 0, 0);
+                    accw[i][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, b1, accw[i][1], 0, 0, 0);
                 }
             }
         }
 
-        // ---------------- data gradient (16x16x32): channels 16w.., 6 row tiles
+        // ---------------- data gradient (16x16x32); two row tiles in flight
 #pragma unroll
-        for (int rt = 0; rt < 6; ++rt) {
-            f32x4 acc = {};
+        for (int rp = 0; rp < 3; ++rp) {
+            f32x4 acc0 = {}, acc1 = {};
+            const char* base0 = X + bd[2 * rp];
+            const char* base1 = X + bd[2 * rp + 1];
 #pragma unroll
             for (int ks = 0; ks < 18; ++ks) {
-                const uint32_t e = da_addr[rt][ks >> 1];
-                const int row = e & 0xffff;
-                const int c = 4 * (ks & 1) + g;  // co chunk: co0 = 32*(ks&1) + 8g
-                const char* src = (e >> 16) ? X + c3::XB + c2_dyaddr(row, c) : zero;
-                const s16x8 a = *(const s16x8*)src;
-                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
-                                                             __builtin_bit_cast(bf16x8, bw[ks]), acc, 0, 0, 0);
+                const int tap = ks >> 1, ky = tap / 3, kx = tap - 3 * ky;
+                const int off = DP * (24 - (11 * ky + kx)) + 64 * (ks & 1);
+                const s16x8 a0 = *(const s16x8*)(base0 + off);
+                const s16x8 a1 = *(const s16x8*)(base1 + off);
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a0),
+                                                              __builtin_bit_cast(bf16x8, bw[ks]), acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a1),
+                                                              __builtin_bit_cast(bf16x8, bw[ks]), acc1, 0, 0, 0);
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int row = rt * 16 + 4 * g + r;
-                outt[row * 64 + 16 * w + (lane & 15)] = (__bf16)acc[r];
+                const int row = rp * 32 + 4 * g + r;
+                outt[row * 64 + 16 * w + (lane & 15)] = (__bf16)acc0[r];
+                if (row + 16 < 81) outt[(row + 16) * 64 + 16 * w + (lane & 15)] = (__bf16)acc1[r];
             }
         }
         lds_barrier();  // dgrad tile complete
@@ -685,9 +630,8 @@ __global__ __launch_bounds__(256, 1) void conv3_bwd_fr(const __bf16* __restrict_
             for (int i = 0; i < (c3::OUT_CH + 255) / 256; ++i) {
                 const int P = threadIdx.x + 256 * i;
                 if (P < c3::OUT_CH) {
-                    const int pix = P >> 3, c = P & 7;
-                    const bf16x8 v = *(const bf16x8*)(outt + pix * 64 + 8 * c);
-                    const bf16x8 m = *(const bf16x8*)(X + c3_xaddr(pix, 8 * c));
+                    const bf16x8 v = *(const bf16x8*)(outt + 8 * P);
+                    const bf16x8 m = *(const bf16x8*)(X + 16 * P);
                     bf16x8 o;
 #pragma unroll
                     for (int j = 0; j < 8; ++j) o[j] = (float)m[j] > 0.f ? v[j] : (__bf16)0.f;
@@ -700,7 +644,7 @@ __global__ __launch_bounds__(256, 1) void conv3_bwd_fr(const __bf16* __restrict_
         int m3 = 0;
         if (it + 3 < nmine) {
             const int fn = blockIdx.x + (it + 3) * gridDim.x;
-            c3_issue(a2 + (size_t)fn * 5184, da3 + (size_t)fn * 3136, lds0 + slot * c3::SLOT, w, lane);
+            c3_issue(a2 + (size_t)fn * 5184, da3 + (size_t)fn * 3136, dvo, lds0 + slot * c3::SLOT, w, lane);
             issued += npw;
             m3 = issued;
         }
@@ -732,10 +676,10 @@ __global__ __launch_bounds__(256, 1) void conv3_bwd_fr(const __bf16* __restrict_
     }
 }
 
-int conv3_bwd_fr_launch(const __bf16* a2, const __bf16* da3, const __bf16* w3d, __bf16* da2,
-                        float* slab, float* cs_slab, int nframes, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(conv3_bwd_fr, dim3(grid), dim3(256), 0, s, a2, da3, w3d, da2, slab, cs_slab,
-                       nframes);
+int conv3_bwd_fr_launch(const __bf16* a2, const __bf16* da3, const __bf16* w3d, __bf16* da2, float* slab,
+                        float* cs_slab, int nframes, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(conv3_bwd_fr, dim3(grid), dim3(256), 0, s, a2, da3, w3d, da2,
+                       slab, cs_slab, nframes);
     FI_HIP_CHECK(hipGetLastError());
     return FI_OK;
 }

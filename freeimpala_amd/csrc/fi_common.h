@@ -77,6 +77,35 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_base) {
         : "memory");
 }
 
+// Raw buffer descriptor (stride 0, range-checked to `bytes`) from wave-uniform inputs.
+typedef int fi_i32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ fi_i32x4 make_rsrc(const void* base, uint32_t bytes) {
+    const uint64_t p = (uint64_t)base;
+    fi_i32x4 r;
+    r[0] = __builtin_amdgcn_readfirstlane((uint32_t)p);
+    r[1] = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+    r[2] = __builtin_amdgcn_readfirstlane(bytes);
+    r[3] = 0x00020000;
+    return r;
+}
+
+// LDS-DMA through a buffer descriptor: lane copies 16 B from byte offset `voff` of the
+// buffer to LDS (lds_base + 16 * lane). Offsets past the descriptor's range read as zero,
+// which the conv backward kernels use for zero borders (FI_OOB).
+constexpr uint32_t FI_OOB = 0x80000000u;
+__device__ __forceinline__ void blds16(fi_i32x4 rsrc, uint32_t voff, uint32_t lds_base) {
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %3\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(rsrc), "s"(lds_base)
+        : "memory");
+}
+
 template <typename T>
 __device__ __forceinline__ uint32_t lds_addr(T* p) {
     return (uint32_t)(uintptr_t)p;
