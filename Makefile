@@ -11,7 +11,7 @@ SRCS := $(CSRC)/vtrace.hip $(CSRC)/gemm_f32.hip $(CSRC)/misc.hip $(CSRC)/atari.h
 OBJS := $(patsubst $(CSRC)/%,$(OBJDIR)/%.o,$(SRCS))
 HDRS := $(wildcard $(CSRC)/*.h) include/fi_learner.h
 
-all: $(LIBDIR)/libfi_learner.so oracle
+all: $(LIBDIR)/libfi_learner.so oracle host
 
 $(OBJDIR)/%.hip.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
@@ -28,6 +28,12 @@ $(LIBDIR)/libfi_learner.so: $(OBJS)
 oracle:
 	$(MAKE) -s -C oracle
 
+# C++ host-side check program (include/freeimpala_amd/device_learner.hpp over the C ABI)
+host: build/host_learner_check
+build/host_learner_check: tests/cpp/host_learner_check.cpp include/freeimpala_amd/device_learner.hpp include/fi_learner.h $(LIBDIR)/libfi_learner.so
+	@mkdir -p build
+	g++ -std=c++17 -O2 -Wall -Iinclude $< -o $@ -L$(LIBDIR) -lfi_learner -pthread '-Wl,-rpath,$$ORIGIN/../$(LIBDIR)' -Wl,-rpath,/opt/rocm/lib
+
 clean:
 	rm -rf build $(LIBDIR)
-.PHONY: all oracle clean
+.PHONY: all oracle host clean

@@ -25,6 +25,8 @@ int vtrace_launch(int variant, int T, int B, int A, const float* pi, const float
                   double* losses, void* ws, size_t ws_bytes, hipStream_t stream,
                   bool finalize = true, int* nblk_out = nullptr);
 int vtrace_finalize_launch(void* ws, int nblk, double* losses, hipStream_t stream);
+// per-workgroup loss partials [nblk][3] inside a vtrace workspace
+const double* vtrace_partials(const void* ws);
 
 // gemm_f32.hip (MLP, exact fp32)
 int f32_linear_fwd(const float* X, int M, int K, const float* W, const float* bias, int N,
@@ -44,7 +46,10 @@ int f32_heads_wgrad_partial(const float* X, int I, const HeadsGrad& g, int split
 int colsum_partial(const float* Y, int M, int N, int splits, float* slab, hipStream_t s);
 int heads_colsum_partial(const HeadsGrad& g, int splits, float* slab, hipStream_t s);
 int reduce_slabs(const float* slab, int splits, size_t count, float* out, hipStream_t s);
-int grad_sqnorm(const float* g, size_t n, double* part, int nblk, double* out, hipStream_t s);
+// squared L2 norm of g -> *out; optionally also sums vt_nblk V-trace loss partials [i][3]
+// into vt_losses[0..2] in the same (final) launch
+int grad_sqnorm(const float* g, size_t n, double* part, int nblk, double* out, hipStream_t s,
+                const double* vt_part = nullptr, int vt_nblk = 0, double* vt_losses = nullptr);
 int optimizer_step(int opt, float* p, const float* g, float* m, float* v, size_t n, float lr,
                    float b1, float b2, float eps, double bc1, double bc2, const double* sqnorm,
                    float max_norm, hipStream_t s);

@@ -444,16 +444,13 @@ static int run_step(fi_learner* l, bool have_host_batch, fi_step_stats* out) {
         FI_TRY(atari_forward(l->atari, l->frames, l->logits, l->values, l->stream, l->profiling ? &tg : nullptr));
     }
     mark(l, FI_PHASE_VTRACE);
+    int vt_nblk = 0;
     {
-        int nblk = 0;
-        {
-            Tag t(l, "vtrace");
-            FI_TRY(vtrace_launch(0, l->T, l->B, l->A, l->logits, l->mu, l->act, l->rew, l->disc,
-                                 l->values, l->cfg.hp, l->vs, l->pg_adv, l->dlogits, l->dvalue,
-                                 l->small, l->vt_ws, l->vt_ws_bytes, l->stream, false, &nblk));
-        }
-        Tag t(l, "vtrace_finalize");
-        FI_TRY(vtrace_finalize_launch(l->vt_ws, nblk, l->small, l->stream));
+        // scan + loss + gradients; the loss partials are summed by the gradient-norm kernel
+        Tag t(l, "vtrace");
+        FI_TRY(vtrace_launch(0, l->T, l->B, l->A, l->logits, l->mu, l->act, l->rew, l->disc,
+                             l->values, l->cfg.hp, l->vs, l->pg_adv, l->dlogits, l->dvalue,
+                             l->small, l->vt_ws, l->vt_ws_bytes, l->stream, false, &vt_nblk));
     }
     mark(l, FI_PHASE_BACKWARD);
     if (l->cfg.arch == FI_ARCH_MLP) FI_TRY(mlp_backward(l));
@@ -471,7 +468,11 @@ static int run_step(fi_learner* l, bool have_host_batch, fi_step_stats* out) {
             return fail(FI_ERR_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
     }
     mark(l, FI_PHASE_OPTIMIZER);
-    { Tag t(l, "grad_norm"); FI_TRY(grad_sqnorm(l->grads, l->nparams, l->small + 8, kSqParts, l->small + 3, l->stream)); }
+    {
+        Tag t(l, "grad_norm");  // + the V-trace loss sums (losses land in small[0..2])
+        FI_TRY(grad_sqnorm(l->grads, l->nparams, l->small + 8, kSqParts, l->small + 3, l->stream,
+                           vtrace_partials(l->vt_ws), vt_nblk, l->small));
+    }
     const int step = l->step_count + 1;
     const double bc1 = 1.0 - std::pow((double)l->cfg.beta1, step);
     const double bc2 = 1.0 - std::pow((double)l->cfg.beta2, step);

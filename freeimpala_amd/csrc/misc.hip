@@ -234,19 +234,40 @@ __global__ void sqnorm_part_kernel(const float* __restrict__ g, size_t n, double
     if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-__global__ void sqnorm_final_kernel(const double* part, int nblk, double* out) {
-    __shared__ double red[4];
-    double s = 0.0;
+__global__ void sqnorm_final_kernel(const double* part, int nblk, double* out, const double* vt_part,
+                                    int vt_nblk, double* vt_losses) {
+    __shared__ double red[4][4];
+    double s = 0.0, l0 = 0.0, l1 = 0.0, l2 = 0.0;
     for (int i = threadIdx.x; i < nblk; i += blockDim.x) s += part[i];
+    for (int i = threadIdx.x; i < vt_nblk; i += blockDim.x) {
+        l0 += vt_part[(size_t)i * 3];
+        l1 += vt_part[(size_t)i * 3 + 1];
+        l2 += vt_part[(size_t)i * 3 + 2];
+    }
     s = wave_sum(s);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    l0 = wave_sum(l0);
+    l1 = wave_sum(l1);
+    l2 = wave_sum(l2);
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = s;
+        red[1][threadIdx.x >> 6] = l0;
+        red[2][threadIdx.x >> 6] = l1;
+        red[3][threadIdx.x >> 6] = l2;
+    }
     __syncthreads();
-    if (threadIdx.x == 0) *out = (red[0] + red[1]) + (red[2] + red[3]);
+    if (threadIdx.x < 4) {
+        const double* r = red[threadIdx.x];
+        const double v = (r[0] + r[1]) + (r[2] + r[3]);
+        if (threadIdx.x == 0) *out = v;
+        else if (vt_losses) vt_losses[threadIdx.x - 1] = v;
+    }
 }
 
-int grad_sqnorm(const float* g, size_t n, double* part, int nblk, double* out, hipStream_t s) {
+int grad_sqnorm(const float* g, size_t n, double* part, int nblk, double* out, hipStream_t s,
+                const double* vt_part, int vt_nblk, double* vt_losses) {
     hipLaunchKernelGGL(sqnorm_part_kernel, dim3(nblk), dim3(256), 0, s, g, n, part);
-    hipLaunchKernelGGL(sqnorm_final_kernel, dim3(1), dim3(256), 0, s, part, nblk, out);
+    hipLaunchKernelGGL(sqnorm_final_kernel, dim3(1), dim3(256), 0, s, part, nblk, out, vt_part,
+                       vt_losses ? vt_nblk : 0, vt_losses);
     FI_HIP_CHECK(hipGetLastError());
     return FI_OK;
 }

@@ -29,7 +29,25 @@
 
 namespace fi {
 
+#ifdef FI_VT_NOMATH  // timing experiment only: transcendental-free stand-ins
+#define VT_EXP(x) ((x) * 0.5f + 1.f)
+#define VT_LOG(x) ((x) * 0.5f)
+#define VT_EXP2(x) ((x) * 0.5f + 1.f)
+#define VT_LOG2(x) ((x) * 0.5f)
+#else
+#define VT_EXP(x) __expf(x)
+#define VT_LOG(x) __logf(x)
+#define VT_EXP2(x) __builtin_amdgcn_exp2f(x)
+#define VT_LOG2(x) __builtin_amdgcn_logf(x)
+#endif
+#ifdef FI_VT_NT
+#define VT_ST(v, p) __builtin_nontemporal_store((v), (p))
+#else
+#define VT_ST(v, p) (*(p) = (v))
+#endif
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 struct VtArgs {
     int T, B, A;
@@ -48,7 +66,11 @@ struct VtArgs {
     fi_vtrace_hparams hp;
 };
 
+#ifdef FI_VT_STAMPS
+constexpr size_t kSinkFloats = 2048 + 2 * 20 * 1024;  // + stamps of up to 1024 workgroups
+#else
 constexpr size_t kSinkFloats = 2048;
+#endif
 
 __device__ __forceinline__ void block_reduce3(double pg, double base, double ent, double* red,
                                               double* out) {
@@ -129,61 +151,79 @@ __global__ __launch_bounds__(256) void vtrace_column_kernel(VtArgs a) {
 }
 
 // ------------------------------------------------------------------------------------
-// Kernel 1: LDS-staged reverse-time chunks, LDS-DMA ring, shuffle scan
+// Kernel 1: LDS-staged reverse-time chunks, LDS-DMA double buffer, shuffle scan.
+// Workgroup = 8 batch columns x all T, 256 threads, two workgroups per CU (81,920 B of LDS
+// each) so one workgroup's arithmetic overlaps the other's DMA waits. A chunk is 32
+// timesteps; wave w owns rows 8w..8w+7 of it (lane = 8 * row + column), reads only its own
+// rows of the logits tiles, writes its dlogits back over its own pi rows and its scan total
+// over its own mu rows, and stores its own dlogits rows -- so a chunk needs two barriers
+// (data landed, wave totals visible). Pieces of the partial (earliest) chunk that hold no
+// valid timestep are not fetched.
 // ------------------------------------------------------------------------------------
+#ifndef FI_VT_NW
+#define FI_VT_NW 4
+#endif
 template <int A>
 struct VtLayout {
-    static constexpr int NB = 16;                      // batch columns per workgroup
-    static constexpr int TC = 16;                      // timesteps per chunk
+    static constexpr int NW = FI_VT_NW;                // waves per workgroup (8 rows each)
+    static constexpr int NB = 8;                       // batch columns per workgroup
+    static constexpr int TC = 8 * NW;                  // timesteps per chunk
     static constexpr int ROWF = NB * A;                // floats per t-row of a logits tile
-    static constexpr int ROW4 = ROWF / 4;              // float4 per t-row (= 4A)
-    static constexpr int LOGB = TC * ROWF * 4;         // bytes per logits tile (= 1024*A)
-    static constexpr int SCB = TC * NB * 4;            // bytes per scalar tile (= 1 KiB)
+    static constexpr int ROWB = ROWF * 4;              // bytes per t-row (= 32A)
+    static constexpr int LOGB = TC * ROWB;             // bytes per logits tile (= 256*NW*A)
+    static constexpr int SCB = TC * NB * 4;            // bytes per scalar tile (= 256*NW)
+    static constexpr int PT = LOGB / 1024;             // 1-KiB pieces per logits tile
     static constexpr int SLOT = 2 * LOGB + 4 * SCB;    // pi | mu | act | rew | disc | val
-    static constexpr int RING = 3;                     // chunks in flight
-    static constexpr int OFF_DLOG = RING * SLOT;       // dlogits staging tile
-    static constexpr int OFF_SMALL = OFF_DLOG + LOGB;  // carry/vnext/wave totals/reduce
-    static constexpr int SMALL = (2 * NB + 2 * NB + 4 * NB + 4 * NB) * 4 + 4 * 3 * 8;
-    static constexpr int TOTAL = OFF_SMALL + SMALL;
-    static constexpr int NINSTR = 2 * A + 4;           // 1-KiB LDS-DMA pieces per chunk
-    static constexpr int G = NINSTR / 4;               // per wave
+    static constexpr int RING = 2;
+    static constexpr int TOTAL = RING * SLOT;
+    static constexpr int GLOG = 2 * PT / NW;           // logits pieces per wave per chunk
+    static constexpr int WPS0 = (163840 / TOTAL) * NW / 4;  // waves per SIMD the LDS allows
+    static constexpr int WPS = WPS0 < 1 ? 1 : (WPS0 > 8 ? 8 : WPS0);
     static_assert(A % 2 == 0, "fast V-trace kernel needs even A");
+    static_assert((NW == 2 || NW == 4) && LOGB % 1024 == 0 && (2 * PT) % NW == 0, "tiling");
     static_assert(TOTAL <= 160 * 1024, "LDS budget");
 };
 
-template <int A>
-__device__ __forceinline__ void vt_issue_chunk(const VtArgs& a, uint32_t lds0, int slot, int t0,
-                                               int b0, int w, int lane) {
+// queue chunk (rows t0 .. t0+31) into ring slot `slot`; returns the pieces this wave issued
+// (pieces I0 <= i < I1 of this wave's list: logits pieces 0..GLOG-1, then its scalar piece;
+// the list is issued in groups between arithmetic so the TA drains between them)
+template <int A, int I0, int I1>
+__device__ __forceinline__ int vt_issue_chunk(const VtArgs& a, uint32_t lds0, int slot, int t0,
+                                              int b0, int w, int lane) {
     using L = VtLayout<A>;
     const uint32_t base = lds0 + (uint32_t)(slot * L::SLOT);
+    const int first_row = t0 < 0 ? -t0 : 0;  // rows above hold t < 0: not needed
+    int n = 0;
 #pragma unroll
-    for (int i = 0; i < L::G; ++i) {
-        const int j = w + 4 * i;  // wave-uniform piece index
-        if (j < 2 * A) {
-            const int which = j >= A ? 1 : 0;
-            const int jj = j - which * A;
-            const int q = jj * 64 + lane;  // float4 index inside the [TC][ROW4] tile
-            const int tl = q / L::ROW4, c4 = q - tl * L::ROW4;
-            const int t = max(t0 + tl, 0);
-            const float* arr = which ? a.mu : a.pi;
-            const float* src = arr + ((size_t)t * a.B + b0) * A + c4 * 4;
-            glds16(src, base + which * L::LOGB + jj * 1024);
-        } else {
-            const int s = j - 2 * A;  // 0 act, 1 rew, 2 disc, 3 val
-            const int tl = lane >> 2, qd = lane & 3;
-            const int t = max(t0 + tl, 0);
-            const char* arr = s == 0 ? (const char*)a.act
-                              : s == 1 ? (const char*)a.rew
-                              : s == 2 ? (const char*)a.disc
-                                       : (const char*)a.val;
-            const char* src = arr + ((size_t)t * a.B + b0) * 4 + qd * 16;
-            glds16(src, base + 2 * L::LOGB + s * L::SCB);
-        }
+    for (int i = I0; i < (I1 < L::GLOG ? I1 : L::GLOG); ++i) {
+        const int j = w + L::NW * i;  // wave-uniform piece index: pi (0..PT-1), mu (PT..2PT-1)
+        const int jj = j < L::PT ? j : j - L::PT;
+        const int last_row = (jj * 1024 + 1023) / L::ROWB;
+        if (last_row < first_row) continue;
+        const int q = jj * 1024 + 16 * lane;  // byte inside the tile
+        const int tl = q / L::ROWB, cb = q - tl * L::ROWB;
+        const int t = max(t0 + tl, 0);
+        const float* arr = j < L::PT ? a.pi : a.mu;
+        glds16((const char*)(arr + ((size_t)t * a.B + b0) * A) + cb, base + (j < L::PT ? 0 : L::LOGB) + jj * 1024);
+        ++n;
     }
+    if (I1 > L::GLOG) {  // scalar tiles (TC rows x 8 columns x 4 B): wave w's piece holds 4/NW of them,
+       // lane -> (tile, row, 16-B half of the row)
+        constexpr int LPT = 16 * L::NW;  // lanes per tile
+        const int s = w * (4 / L::NW) + lane / LPT;
+        const int t = max(t0 + ((lane % LPT) >> 1), 0);
+        const char* arr = s == 0 ? (const char*)a.act
+                          : s == 1 ? (const char*)a.rew
+                          : s == 2 ? (const char*)a.disc
+                                   : (const char*)a.val;
+        glds16(arr + ((size_t)t * a.B + b0) * 4 + (lane & 1) * 16, base + 2 * L::LOGB + w * 1024);
+        ++n;
+    }
+    return n;
 }
 
 template <int A>
-__global__ __launch_bounds__(256, 1) void vtrace_lds_kernel(VtArgs a) {
+__global__ __launch_bounds__(64 * VtLayout<A>::NW, VtLayout<A>::WPS) void vtrace_lds_kernel(VtArgs a) {
     using L = VtLayout<A>;
     __shared__ __attribute__((aligned(16))) char smem[L::TOTAL];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -192,51 +232,42 @@ __global__ __launch_bounds__(256, 1) void vtrace_lds_kernel(VtArgs a) {
     const int b0 = cb * L::NB;
     const int T = a.T, B = a.B;
     const int nchunks = (T + L::TC - 1) / L::TC;
-    const int tl = w * 4 + (lane >> 4), c = lane & 15;
+    const int r = lane >> 3, c = lane & 7;
+    const int tl = 8 * w + r;
     const int b = b0 + c;
     const uint32_t lds0 = lds_addr(smem);
 
-    float* carry = (float*)(smem + L::OFF_SMALL);  // [2][NB]
-    float* vnext = carry + 2 * L::NB;              // [2][NB]
-    float* totd = vnext + 2 * L::NB;               // [4][NB]
-    float* totg = totd + 4 * L::NB;                // [4][NB]
-    double* red = (double*)(totg + 4 * L::NB);     // [4][3]
-    float* dstage = (float*)(smem + L::OFF_DLOG);
+    float vnext = a.val[(size_t)T * B + b];  // V at the row after the chunk (bootstrap first)
+    float carry = 0.f;                       // acc at the row after the chunk
+    if (tid < L::NB) a.dval[(size_t)T * B + b0 + tid] = 0.f;
 
-    if (tid < L::NB) {
-        carry[tid] = 0.f;
-        vnext[tid] = a.val[(size_t)T * B + b0 + tid];  // bootstrap V_T
-        a.dval[(size_t)T * B + b0 + tid] = 0.f;
-    }
-
-    // prologue: up to RING chunks in flight; marks = VMEM ops issued after each chunk
-    int issued = 0, m0 = 0, m1 = 0, m2 = 0;
-    vt_issue_chunk<A>(a, lds0, 0, T - L::TC, b0, w, lane);
-    issued += L::G;
-    m0 = issued;
-    if (nchunks > 1) {
-        vt_issue_chunk<A>(a, lds0, 1, T - 2 * L::TC, b0, w, lane);
-        issued += L::G;
-        m1 = issued;
-    }
-    if (nchunks > 2) {
-        vt_issue_chunk<A>(a, lds0, 2, T - 3 * L::TC, b0, w, lane);
-        issued += L::G;
-        m2 = issued;
-    }
-    const int n_dst = (A - w + 3) / 4;  // dlogits float4 stores per wave per chunk
+    constexpr int NP = L::GLOG + 1, G1 = NP / 3, G2 = 2 * NP / 3;  // issue groups
+    int issued = vt_issue_chunk<A, 0, NP>(a, lds0, 0, T - L::TC, b0, w, lane);
+    int mark = issued;  // VMEM ops issued once the chunk being waited for was queued
     const fi_vtrace_hparams hp = a.hp;
 
     float pg = 0.f, base = 0.f, ent = 0.f;
+#ifdef FI_VT_STAMPS  // timing experiment: s_memrealtime stamps of wave 0, written over vs
+    unsigned long long stamp[20];
+    int ns = 0;
+    stamp[ns++] = __builtin_amdgcn_s_memrealtime();
+#define VT_STAMP() if (ns < 20) stamp[ns++] = __builtin_amdgcn_s_memrealtime()
+#else
+#define VT_STAMP()
+#endif
     for (int k = 0; k < nchunks; ++k) {
-        const int slot = k % 3;
+        const int slot = k & 1;
         const int t0 = T - L::TC * (k + 1);
-        wait_vmcnt(issued - m0);
-        lds_barrier();  // B1: chunk k landed for every wave
-
-        const char* sl = smem + slot * L::SLOT;
-        const float* zpi = (const float*)sl + tl * L::ROWF + c * A;
-        const float* zmu = (const float*)(sl + L::LOGB) + tl * L::ROWF + c * A;
+        wait_vmcnt(issued - mark);
+        lds_barrier();  // B1: chunk k landed for every wave; slot (k+1)&1 fully consumed
+        VT_STAMP();
+        const bool more = k + 1 < nchunks;
+        if (more) issued += vt_issue_chunk<A, 0, G1>(a, lds0, slot ^ 1, t0 - L::TC, b0, w, lane);
+        VT_STAMP();
+#ifndef FI_VT_DMAONLY
+        char* sl = smem + slot * L::SLOT;
+        float* zpi = (float*)sl + tl * L::ROWF + c * A;
+        float* zmu = (float*)(sl + L::LOGB) + tl * L::ROWF + c * A;
         const int* sact = (const int*)(sl + 2 * L::LOGB);
         const float* srew = (const float*)(sl + 2 * L::LOGB + L::SCB);
         const float* sdisc = (const float*)(sl + 2 * L::LOGB + 2 * L::SCB);
@@ -244,131 +275,157 @@ __global__ __launch_bounds__(256, 1) void vtrace_lds_kernel(VtArgs a) {
         const int t = t0 + tl;
         const bool valid = t >= 0;
 
-        float zp[A], zm[A];
+        // packed-fp32 softmax statistics: e_i = 2^(z_i log2e - max log2e) (one v_pk_fma +
+        // one v_exp_f32 per logit), pi_i = e_i / sum e, H = sum pi log pi = (sum e z)/sum e - lse
+        constexpr float L2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
+        f32x2 zp2[A / 2], zm2[A / 2];
 #pragma unroll
-        for (int i = 0; i < A; i += 2) {
-            const float2 p2 = *(const float2*)(zpi + i);
-            const float2 m2v = *(const float2*)(zmu + i);
-            zp[i] = p2.x; zp[i + 1] = p2.y;
-            zm[i] = m2v.x; zm[i + 1] = m2v.y;
+        for (int i = 0; i < A / 2; ++i) {
+            zp2[i] = *(const f32x2*)(zpi + 2 * i);
+            zm2[i] = *(const f32x2*)(zmu + 2 * i);
         }
         int at = sact[tl * L::NB + c];
         at = at < 0 ? 0 : (at >= A ? A - 1 : at);
-        const float r = srew[tl * L::NB + c];
+        const float zpa = zpi[at], zma = zmu[at];
+        const float rw = srew[tl * L::NB + c];
         const float g = sdisc[tl * L::NB + c];
         const float v = sval[tl * L::NB + c];
-        const float vn = (tl == L::TC - 1) ? vnext[(k & 1) * L::NB + c] : sval[(tl + 1) * L::NB + c];
+        const float vn = (tl == L::TC - 1) ? vnext : sval[(tl + 1) * L::NB + c];
+        const float vrow0 = sval[c];  // V at this chunk's first row: next chunk's vnext
 
-        float mx = zp[0], mm = zm[0];
+        float mx = fmaxf(zp2[0].x, zp2[0].y), mm = fmaxf(zm2[0].x, zm2[0].y);
 #pragma unroll
-        for (int i = 1; i < A; ++i) { mx = fmaxf(mx, zp[i]); mm = fmaxf(mm, zm[i]); }
-        float sp = 0.f, sm = 0.f;
-#pragma unroll
-        for (int i = 0; i < A; ++i) { sp += expf(zp[i] - mx); sm += expf(zm[i] - mm); }
-        const float lse = mx + logf(sp), lsem = mm + logf(sm);
-        float zpa = 0.f, zma = 0.f;
-#pragma unroll
-        for (int i = 0; i < A; ++i) {
-            zpa = (i == at) ? zp[i] : zpa;
-            zma = (i == at) ? zm[i] : zma;
+        for (int i = 1; i < A / 2; ++i) {
+            mx = fmaxf(mx, fmaxf(zp2[i].x, zp2[i].y));
+            mm = fmaxf(mm, fmaxf(zm2[i].x, zm2[i].y));
         }
+        const f32x2 nmx = {-mx * L2E, -mx * L2E}, nmm = {-mm * L2E, -mm * L2E};
+        f32x2 e2[A / 2];
+        f32x2 sp2 = {0.f, 0.f}, sm2 = {0.f, 0.f}, sz2 = {0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < A / 2; ++i) {
+            const f32x2 ap = zp2[i] * L2E + nmx;
+            const f32x2 am = zm2[i] * L2E + nmm;
+            e2[i] = f32x2{VT_EXP2(ap.x), VT_EXP2(ap.y)};
+            sp2 += e2[i];
+            sz2 += e2[i] * zp2[i];
+            sm2 += f32x2{VT_EXP2(am.x), VT_EXP2(am.y)};
+        }
+        if (more) issued += vt_issue_chunk<A, G1, G2>(a, lds0, slot ^ 1, t0 - L::TC, b0, w, lane);
+        const float sp = sp2.x + sp2.y, sm = sm2.x + sm2.y;
+        const float lse = mx + VT_LOG2(sp) * LN2, lsem = mm + VT_LOG2(sm) * LN2;
+        const float inv = __builtin_amdgcn_rcpf(sp);
+        const float plogp = (sz2.x + sz2.y) * inv - lse;
         const float lpa = zpa - lse, lma = zma - lsem;
-        const float ratio = expf(lpa - lma);
+        const float ratio = VT_EXP(lpa - lma);
         const float rho = fminf(hp.rho_bar, ratio);
         const float cc = hp.lambda_ * fminf(hp.c_bar, ratio);
         const float pgr = fminf(hp.pg_rho_bar, ratio);
-        float d = valid ? rho * (r + g * vn - v) : 0.f;
+        float d = valid ? rho * (rw + g * vn - v) : 0.f;
         float gg = valid ? g * cc : 1.f;
 
-        // inclusive suffix composition over the wave's 4 timesteps (lanes +16, +32)
-        {
-            const float d2 = __shfl_down(d, 16, 64), g2 = __shfl_down(gg, 16, 64);
-            if (lane < 48) { d = d + gg * d2; gg = gg * g2; }
+        // inclusive suffix composition over the wave's 8 rows (lanes +8, +16, +32)
+#pragma unroll
+        for (int s = 8; s < 64; s <<= 1) {
+            const float d2 = __shfl_down(d, s, 64), g2 = __shfl_down(gg, s, 64);
+            if (lane + s < 64) { d = d + gg * d2; gg = gg * g2; }
         }
-        {
-            const float d2 = __shfl_down(d, 32, 64), g2 = __shfl_down(gg, 32, 64);
-            if (lane < 32) { d = d + gg * d2; gg = gg * g2; }
-        }
-        if (lane < 16) {
-            totd[w * L::NB + c] = d;
-            totg[w * L::NB + c] = gg;
+        if (more) issued += vt_issue_chunk<A, G2, NP>(a, lds0, slot ^ 1, t0 - L::TC, b0, w, lane);
+        mark = issued;  // the wait for chunk k+1 ignores the stores issued after this point
+        // wave total -> this wave's own first mu row (no other wave reads it)
+        float* tot = (float*)(sl + L::LOGB) + (8 * w) * L::ROWF;
+        if (lane < 8) {
+            tot[c] = d;
+            tot[8 + c] = gg;
         }
         lds_barrier();  // B2: wave totals visible
+        VT_STAMP();
 
-        float acc_in = carry[(k & 1) * L::NB + c];  // acc at t0 + 16
-        for (int w2 = 3; w2 > w; --w2) acc_in = totd[w2 * L::NB + c] + totg[w2 * L::NB + c] * acc_in;
+        float acc_in = carry;  // acc at row 8(w+1): compose the later waves onto the carry
+        float carry_new = carry;
+#pragma unroll
+        for (int w2 = L::NW - 1; w2 >= 0; --w2) {
+            const float* t2 = (const float*)(sl + L::LOGB) + (8 * w2) * L::ROWF;
+            carry_new = t2[c] + t2[8 + c] * carry_new;
+            if (w2 == w + 1) acc_in = carry_new;
+        }
+        if (w == L::NW - 1) acc_in = carry;
         const float acc = d + gg * acc_in;
-        const float acc_up = __shfl_down(acc, 16, 64);
-        const float acc_nx = (lane >= 48) ? acc_in : acc_up;
+        const float acc_up = __shfl_down(acc, 8, 64);
+        const float acc_nx = (r == 7) ? acc_in : acc_up;
         const float vs_t = v + acc;
         const float vs_n = vn + acc_nx;
-        const float adv = pgr * (r + g * vs_n - v);
+        const float adv = pgr * (rw + g * vs_n - v);
         const float dv = -hp.baseline_cost * acc;
+        carry = carry_new;
+        vnext = vrow0;
 
-        float plogp = 0.f;
+        // dlogits over this wave's own pi rows:
+        //   dz_i = pi_i (adv + ec (log pi_i - H)) - adv [i = a_t] = e_i (alpha + beta z_i) - adv [i = a_t]
+        {
+            const float ec = hp.entropy_cost;
+            const float al = inv * (adv - ec * (plogp + lse)), be = inv * ec;
+            const f32x2 al2 = {al, al};
 #pragma unroll
-        for (int i = 0; i < A; ++i) {
-            const float lp = zp[i] - lse;
-            plogp += expf(lp) * lp;
-        }
-        float* dz = dstage + tl * L::ROWF + c * A;
-#pragma unroll
-        for (int i = 0; i < A; i += 2) {
-            float2 o;
-            {
-                const float lp = zp[i] - lse, p = expf(lp);
-                o.x = -adv * ((i == at ? 1.f : 0.f) - p) + hp.entropy_cost * p * (lp - plogp);
-            }
-            {
-                const float lp = zp[i + 1] - lse, p = expf(lp);
-                o.y = -adv * ((i + 1 == at ? 1.f : 0.f) - p) + hp.entropy_cost * p * (lp - plogp);
-            }
-            *(float2*)(dz + i) = o;
+            for (int i = 0; i < A / 2; ++i) *(f32x2*)(zpi + 2 * i) = e2[i] * (zp2[i] * be + al2);
+            zpi[at] -= adv;
         }
         if (valid) {
             pg += -adv * lpa;
             base += 0.5f * acc * acc;
             ent += plogp;
         }
-        {  // always-executed stores (masked rows go to the sink) keep vmcnt counts exact
-            const size_t e = (size_t)(valid ? t : 0) * B + b;
-            float* pvs = valid ? a.vs + e : a.sink + tid;
-            float* padv = valid ? a.adv + e : a.sink + 256 + tid;
-            float* pdv = valid ? a.dval + e : a.sink + 512 + tid;
-            __builtin_nontemporal_store(vs_t, pvs);
-            __builtin_nontemporal_store(adv, padv);
-            __builtin_nontemporal_store(dv, pdv);
-            issued += 3;
+#ifndef FI_VT_NOSTORE
+        // Stores. Every chunk but the last (the only one holding t < 0) stores with the full
+        // wave, so the per-wave VMEM count used by the next chunk's wait is exact; the last
+        // chunk masks freely (nothing waits on its count). Rows: vs/pg_adv/dvalue 32 B per
+        // t-row of the block, merged with the neighbouring blocks' segments in L2.
+        if (valid) {
+            const size_t e = (size_t)t * B + b;
+            VT_ST(vs_t, a.vs + e);
+            VT_ST(adv, a.adv + e);
+            VT_ST(dv, a.dval + e);
         }
-        if (tl == 0) {
-            carry[((k + 1) & 1) * L::NB + c] = acc;
-            vnext[((k + 1) & 1) * L::NB + c] = v;
+        issued += 3;
+        {  // this wave's 8 dlogits rows (8 * 2A float4 = 4 full-wave x4 stores + one x2)
+            const float* srcf = (const float*)sl + (8 * w) * L::ROWF;
+            float* dst0 = a.dlog + ((size_t)(t0 + 8 * w) * B + b0) * A;  // row stride B*A
+            constexpr int N4 = 8 * L::ROWF / 4, NF4 = N4 / 64;         // 288, 4 (A = 18)
+            constexpr int R4 = L::ROWF / 4;                            // float4 per row
+#pragma unroll
+            for (int i = 0; i < NF4; ++i) {
+                const int q = i * 64 + lane, rr = q / R4, c4 = q - rr * R4;
+                if (t0 + 8 * w + rr >= 0)
+                    VT_ST(((const f32x4*)srcf)[q], (f32x4*)(dst0 + (size_t)rr * B * A) + c4);
+            }
+            issued += NF4;
+            constexpr int REM2 = (N4 - NF4 * 64) * 2;  // remaining float2 (0..126)
+            if constexpr (REM2 > 0) {
+#pragma unroll
+                for (int i = 0; i < (REM2 + 63) / 64; ++i) {
+                    const int q2 = NF4 * 128 + i * 64 + lane;  // float2 index
+                    const int rr = q2 / (2 * R4), c2 = q2 - rr * 2 * R4;
+                    if (i * 64 + lane < REM2 && t0 + 8 * w + rr >= 0)
+                        VT_ST(((const f32x2*)srcf)[q2], (f32x2*)(dst0 + (size_t)rr * B * A) + c2);
+                }
+                issued += (REM2 + 63) / 64;
+            }
         }
-        lds_barrier();  // B3: dlogits staged; ring slot k%3 is free
-
-        // dlogits: LDS -> coalesced 16-byte stores (one (t, 16 columns) row = 4A float4)
-        for (int q = tid; q < 64 * A; q += 256) {
-            const int rtl = q / L::ROW4, c4 = q - rtl * L::ROW4;
-            const int rt = t0 + rtl;
-            const f32x4 val = ((const f32x4*)dstage)[q];
-            f32x4* dst = rt >= 0 ? (f32x4*)(a.dlog + ((size_t)rt * B + b0) * A) + c4
-                                 : (f32x4*)(a.sink + 1024) + tid;
-            __builtin_nontemporal_store(val, dst);
-        }
-        issued += n_dst;
-
-        int m3 = 0;
-        if (k + 3 < nchunks) {
-            vt_issue_chunk<A>(a, lds0, slot, T - L::TC * (k + 4), b0, w, lane);
-            issued += L::G;
-            m3 = issued;
-        }
-        m0 = m1;
-        m1 = m2;
-        m2 = m3;
+#endif
+#endif  // FI_VT_DMAONLY
+        VT_STAMP();
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    block_reduce3((double)pg, (double)base, (double)ent, red, a.part + (size_t)blockIdx.x * 3);
+    VT_STAMP();
+#ifdef FI_VT_STAMPS
+    if (tid == 0)
+        for (int i = 0; i < 20; ++i) ((unsigned long long*)(a.sink + 2048))[blockIdx.x * 20 + i] = i < ns ? stamp[i] : 0ull;
+#endif
+    __syncthreads();
+    // per-workgroup loss partials; summed in a fixed order by vtrace_finalize_kernel or, in
+    // the learner step, by the gradient-norm kernel that runs anyway (no extra launch, no
+    // serial tail at the end of this kernel)
+    block_reduce3((double)pg, (double)base, (double)ent, (double*)smem, a.part + (size_t)blockIdx.x * 3);
 }
 
 __global__ __launch_bounds__(256) void vtrace_finalize_kernel(const double* __restrict__ part,
@@ -386,7 +443,7 @@ __global__ __launch_bounds__(256) void vtrace_finalize_kernel(const double* __re
 // ------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------
-static size_t vt_nblk_max(int B) { return (size_t)std::max((B + 15) / 16, (B + 255) / 256); }
+static size_t vt_nblk_max(int B) { return (size_t)std::max((B + 7) / 8, (B + 255) / 256); }
 
 size_t vtrace_workspace_bytes(int T, int B, int A) {
     (void)T;
@@ -396,10 +453,10 @@ size_t vtrace_workspace_bytes(int T, int B, int A) {
 
 template <int A>
 static void launch_lds(const VtArgs& a, int nblk, hipStream_t s) {
-    hipLaunchKernelGGL(vtrace_lds_kernel<A>, dim3(nblk), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(vtrace_lds_kernel<A>, dim3(nblk), dim3(64 * VtLayout<A>::NW), 0, s, a);
 }
 
-static bool lds_supported(int A, int B) { return B % 16 == 0 && A % 2 == 0 && A >= 2 && A <= 20; }
+static bool lds_supported(int A, int B) { return B % 8 == 0 && A % 2 == 0 && A >= 2 && A <= 20; }
 
 int vtrace_launch(int variant, int T, int B, int A, const float* pi, const float* mu,
                   const int32_t* act, const float* rew, const float* disc, const float* val,
@@ -407,8 +464,8 @@ int vtrace_launch(int variant, int T, int B, int A, const float* pi, const float
                   double* losses, void* ws, size_t ws_bytes, hipStream_t stream, bool finalize,
                   int* nblk_out) {
     FI_REQUIRE(T >= 1 && B >= 1 && A >= 1 && A <= 64, "vtrace: bad shape");
-    FI_REQUIRE(pi && mu && act && rew && disc && val && dlog && dval && losses && ws,
-               "vtrace: null pointer");
+    FI_REQUIRE(pi && mu && act && rew && disc && val && dlog && dval && ws, "vtrace: null pointer");
+    finalize = finalize && losses;  // losses == NULL: partials stay in the workspace
     FI_REQUIRE(ws_bytes >= vtrace_workspace_bytes(T, B, A), "vtrace: workspace too small");
     VtArgs a;
     a.T = T; a.B = B; a.A = A;
@@ -418,14 +475,14 @@ int vtrace_launch(int variant, int T, int B, int A, const float* pi, const float
     a.part = (double*)((char*)ws + kSinkFloats * sizeof(float));
     a.hp = hp;
     bool use_lds = variant == 1 || (variant == 0 && lds_supported(A, B));
-    FI_REQUIRE(!(variant == 1 && !lds_supported(A, B)), "vtrace: LDS kernel needs B%16==0, even A<=20");
+    FI_REQUIRE(!(variant == 1 && !lds_supported(A, B)), "vtrace: LDS kernel needs B%8==0, even A<=20");
     int nblk;
     if (use_lds) {
         FI_REQUIRE(vs && adv, "vtrace: LDS kernel writes vs and pg_adv (non-null)");
         FI_REQUIRE(((uintptr_t)pi | (uintptr_t)mu | (uintptr_t)dlog) % 16 == 0 &&
                    ((uintptr_t)act | (uintptr_t)rew | (uintptr_t)disc | (uintptr_t)val) % 16 == 0,
                    "vtrace: LDS kernel needs 16-byte aligned tensors");
-        nblk = B / 16;
+        nblk = B / 8;
         switch (A) {
             case 2: launch_lds<2>(a, nblk, stream); break;
             case 4: launch_lds<4>(a, nblk, stream); break;
@@ -447,6 +504,10 @@ int vtrace_launch(int variant, int T, int B, int A, const float* pi, const float
     if (nblk_out) *nblk_out = nblk;
     if (finalize) return vtrace_finalize_launch(ws, nblk, losses, stream);
     return FI_OK;
+}
+
+const double* vtrace_partials(const void* ws) {
+    return (const double*)((const char*)ws + kSinkFloats * sizeof(float));
 }
 
 int vtrace_finalize_launch(void* ws, int nblk, double* losses, hipStream_t stream) {

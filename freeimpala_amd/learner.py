@@ -113,6 +113,38 @@ class DeviceLearner:
         self.sync()
         hip.upload_ptr(p, a)
 
+    def replay_vtrace(self, n: int = 20) -> float:
+        """Mean device ms of the fused V-trace kernel alone: n back-to-back launches of
+        fi_vtrace_loss_fp32 (no loss finalisation) on this learner's resident tensors,
+        HIP events around the burst. Inputs are read-only and the outputs are rewritten with
+        identical values, so the learner state is unchanged."""
+        T, B, A = self.T, self.B, self.A
+        ptr = {k: self.tensor_ptr(k)[0] for k in ("logits", "mu", "actions", "rewards", "discounts",
+                                                   "values", "vs", "pg_adv", "dlogits", "dvalue")}
+        hp = self.cfg.hp
+        wsb = lib().fi_vtrace_workspace_bytes(T, B, A)
+        ws = hip.DeviceBuffer(wsb)
+        stream = self.stream
+
+        def launch():
+            check(lib().fi_vtrace_loss_fp32(
+                T, B, A, ptr["logits"], ptr["mu"], ptr["actions"], ptr["rewards"], ptr["discounts"],
+                ptr["values"], C.byref(hp), ptr["vs"], ptr["pg_adv"], ptr["dlogits"], ptr["dvalue"],
+                None, ws.ptr, wsb, stream), "fi_vtrace_loss_fp32")
+
+        self.sync()
+        for _ in range(3):
+            launch()
+        e0, e1 = hip.Event(), hip.Event()
+        e0.record(stream)
+        for _ in range(n):
+            launch()
+        e1.record(stream)
+        self.sync()
+        ms = e0.elapsed_ms(e1) / n
+        ws.free()
+        return ms
+
     # --- data parallel
     @staticmethod
     def comm_unique_id() -> bytes:

@@ -138,7 +138,9 @@ int fi_learner_sync(fi_learner* l);
 
 /* ---- standalone kernels on device pointers (stream: hipStream_t or NULL) -----------
  * Layouts: pi/mu/dlogits (T,B,A) fp32; actions (T,B) int32; rewards/discounts/vs/pg_adv
- * (T,B) fp32; values/dvalue (T+1,B) fp32; losses_dev: 3 doubles {pg, baseline, entropy}. */
+ * (T,B) fp32; values/dvalue (T+1,B) fp32; losses_dev: 3 doubles {pg, baseline, entropy}.
+ * workspace: fi_vtrace_workspace_bytes() bytes of device scratch (one per stream in flight).
+ * losses_dev may be NULL: the loss sums are then not finalised (one kernel launch only).     */
 size_t fi_vtrace_workspace_bytes(int T, int B, int A);
 int fi_vtrace_loss_fp32(int T, int B, int A, const float* pi_logits, const float* mu_logits,
                         const int32_t* actions, const float* rewards, const float* discounts,

@@ -1,0 +1,219 @@
+// device_learner.hpp -- C++ host side of the MI355X learner step, above the C ABI.
+//
+// What the reference's Learner needs to move its step on-device, with the reference's
+// own vocabulary and signatures:
+//   * LearnerConfig::from_args   -- the learner flags of cmd/freeimpala (reference
+//     cmd/freeimpala/main.cpp: --players, --batch-size, --seq-length, --entry-size) plus
+//     the device-learner hyper-parameters (--learner-arch, --num-actions, --lr, ...).
+//   * DeviceLearner::step(player_index, batch) -- same parameters as
+//     Learner::trainModel (reference include/freeimpala/learner.h:32) and the same
+//     `batch` that SharedBuffer::readBatch returns (data_structures.h:267-300):
+//     M entries of S * ELEMENT_SIZE bytes, record schema in DESIGN.md section 3.
+//   * DeviceLearner::publish(player_index, blob, version) -- the bytes and version that go
+//     into Model::update / ModelManager::updateModel (data_structures.h:134-140, 441-451);
+//     blob size == param_bytes() is the ModelManager model_size.
+// One fi_learner handle per player (the reference runs one worker thread per player,
+// learner.h:158-163): handles own their HIP stream and device memory, so different
+// players may call step() concurrently from their own threads. Failures never throw
+// across step(): it returns false and last_error() holds the message, matching the
+// reference's log-and-continue style (data_structures.h:420-421). Construction throws
+// std::runtime_error when the HIP library or device is unusable -- there is no CPU
+// fallback.
+#pragma once
+
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "fi_learner.h"
+
+namespace freeimpala_amd {
+
+struct LearnerConfig {
+    size_t players = 1;        // --players
+    size_t batch_size = 32;    // --batch-size (M entries per step)
+    size_t seq_length = 100;   // --seq-length (T); entries carry T+1 records
+    size_t entry_size = 0;     // --entry-size in ELEMENT_SIZE units (0: T+1)
+    std::string arch = "mlp";  // --learner-arch mlp|atari
+    int num_actions = 18;      // --num-actions
+    int obs_dim = 128;         // --obs-dim
+    int hidden = 256;          // --hidden
+    std::string optimizer = "adam";  // --optimizer adam|sgd
+    std::string publish = "fp32";    // --publish fp32|bf16
+    float lr = 5e-4f;          // --lr  (reference README.md:112 default)
+    float max_grad_norm = 40.f;      // --max-grad-norm
+    float gamma = 0.99f;       // --gamma (synthetic generator only)
+    fi_vtrace_hparams hp{1.f, 1.f, 1.f, 1.f, 0.5f, 0.01f};
+    std::vector<int> devices{0};     // --devices 0,1,... (player p -> devices[p % n])
+    uint64_t seed = 42;        // --seed (parameter init)
+
+    size_t entry_records() const { return entry_size ? entry_size : seq_length + 1; }
+
+    // Parses the flags above from argv (unknown flags are ignored so the reference's own
+    // parser can own the rest of the command line). Throws std::invalid_argument on a
+    // malformed value.
+    static LearnerConfig from_args(int argc, const char* const* argv) {
+        return from_args(argc, argv, LearnerConfig());
+    }
+    static LearnerConfig from_args(int argc, const char* const* argv, LearnerConfig c) {
+        auto num = [](const std::string& f, const char* v) -> double {
+            char* end = nullptr;
+            const double x = std::strtod(v, &end);
+            if (!v[0] || (end && *end)) throw std::invalid_argument("bad value for " + f + ": " + v);
+            return x;
+        };
+        for (int i = 1; i + 1 < argc; ++i) {
+            const std::string f = argv[i];
+            const char* v = argv[i + 1];
+            bool used = true;
+            if (f == "--players" || f == "-p") c.players = (size_t)num(f, v);
+            else if (f == "--batch-size" || f == "-M") c.batch_size = (size_t)num(f, v);
+            else if (f == "--seq-length") c.seq_length = (size_t)num(f, v);
+            else if (f == "--entry-size" || f == "-S") c.entry_size = (size_t)num(f, v);
+            else if (f == "--learner-arch") c.arch = v;
+            else if (f == "--num-actions") c.num_actions = (int)num(f, v);
+            else if (f == "--obs-dim") c.obs_dim = (int)num(f, v);
+            else if (f == "--hidden") c.hidden = (int)num(f, v);
+            else if (f == "--optimizer") c.optimizer = v;
+            else if (f == "--publish") c.publish = v;
+            else if (f == "--lr") c.lr = (float)num(f, v);
+            else if (f == "--max-grad-norm") c.max_grad_norm = (float)num(f, v);
+            else if (f == "--gamma") c.gamma = (float)num(f, v);
+            else if (f == "--seed") c.seed = (uint64_t)num(f, v);
+            else if (f == "--devices") {
+                c.devices.clear();
+                std::string s = v;
+                size_t p = 0;
+                while (p <= s.size()) {
+                    const size_t q = s.find(',', p);
+                    const std::string tok = s.substr(p, q == std::string::npos ? std::string::npos : q - p);
+                    if (!tok.empty()) c.devices.push_back((int)num(f, tok.c_str()));
+                    if (q == std::string::npos) break;
+                    p = q + 1;
+                }
+                if (c.devices.empty()) throw std::invalid_argument("--devices: empty list");
+            } else used = false;
+            if (used) ++i;
+        }
+        if (c.players == 0 || c.batch_size == 0 || c.seq_length == 0)
+            throw std::invalid_argument("--players, --batch-size and --seq-length must be > 0");
+        if (c.entry_records() < c.seq_length + 1)
+            throw std::invalid_argument("--entry-size must hold seq_length + 1 records");
+        if (c.arch != "mlp" && c.arch != "atari") throw std::invalid_argument("--learner-arch: mlp|atari");
+        if (c.optimizer != "adam" && c.optimizer != "sgd") throw std::invalid_argument("--optimizer: adam|sgd");
+        if (c.publish != "fp32" && c.publish != "bf16") throw std::invalid_argument("--publish: fp32|bf16");
+        return c;
+    }
+
+    // The C-ABI configuration of player p's handle.
+    fi_learner_config abi_config(size_t p) const {
+        fi_learner_config k;
+        fi_learner_config_init(&k);
+        k.arch = arch == "atari" ? FI_ARCH_ATARI : FI_ARCH_MLP;
+        k.seq_len = (int32_t)seq_length;
+        k.batch = (int32_t)batch_size;
+        k.num_actions = num_actions;
+        k.obs_dim = obs_dim;
+        k.hidden = hidden;
+        k.optimizer = optimizer == "sgd" ? FI_OPT_SGD : FI_OPT_ADAM;
+        k.publish_dtype = publish == "bf16" ? FI_PUBLISH_BF16 : FI_PUBLISH_FP32;
+        k.device = devices[p % devices.size()];
+        k.gamma = gamma;
+        k.hp = hp;
+        k.lr = lr;
+        k.max_grad_norm = max_grad_norm;
+        k.seed = seed + p;
+        return k;
+    }
+};
+
+class DeviceLearner {
+public:
+    explicit DeviceLearner(const LearnerConfig& cfg) : cfg_(cfg), stats_(cfg.players), err_(cfg.players) {
+        if (fi_abi_version() != FI_ABI_VERSION)
+            throw std::runtime_error("libfi_learner ABI version mismatch");
+        handles_.resize(cfg.players, nullptr);
+        for (size_t p = 0; p < cfg.players; ++p) {
+            const fi_learner_config k = cfg.abi_config(p);
+            if (fi_learner_create(&k, &handles_[p]) != FI_OK) {
+                const std::string msg = std::string("fi_learner_create(player ") + std::to_string(p) +
+                                        "): " + fi_last_error();
+                release();
+                throw std::runtime_error(msg);
+            }
+        }
+    }
+    ~DeviceLearner() { release(); }
+    DeviceLearner(const DeviceLearner&) = delete;
+    DeviceLearner& operator=(const DeviceLearner&) = delete;
+
+    // Learner::step(player_index, batch): the body of Learner::trainModel on the device.
+    bool step(size_t player_index, const std::vector<std::vector<char>>& batch) {
+        if (player_index >= handles_.size()) return fail(0, "player_index out of range");
+        if (batch.empty()) return fail(player_index, "empty batch");
+        const size_t eb = batch[0].size();
+        std::vector<const void*> ptrs(batch.size());
+        for (size_t i = 0; i < batch.size(); ++i) {
+            if (batch[i].size() != eb) return fail(player_index, "entries of different sizes");
+            ptrs[i] = batch[i].data();
+        }
+        fi_step_stats st{};
+        if (fi_learner_step(handles_[player_index], ptrs.data(), ptrs.size(), eb, &st) != FI_OK)
+            return fail(player_index, fi_last_error());
+        stats_[player_index] = st;
+        return true;
+    }
+
+    // Parameters of player p as the published Model blob (fp32 or bf16, little endian,
+    // DESIGN.md section 3 order); resizes `blob` to param_bytes().
+    bool publish(size_t p, std::vector<char>& blob, uint64_t& version) {
+        if (p >= handles_.size()) return fail(0, "player_index out of range");
+        blob.resize(param_bytes());
+        if (fi_learner_get_params(handles_[p], blob.data(), blob.size(), &version) != FI_OK)
+            return fail(p, fi_last_error());
+        return true;
+    }
+    // --starting-model resume (Model::loadFromDisk bytes + version).
+    bool load(size_t p, const std::vector<char>& blob, uint64_t version) {
+        if (p >= handles_.size()) return fail(0, "player_index out of range");
+        if (fi_learner_set_params(handles_[p], blob.data(), blob.size(), version) != FI_OK)
+            return fail(p, fi_last_error());
+        return true;
+    }
+
+    size_t param_bytes() const { return fi_learner_param_bytes(handles_[0]); }
+    size_t entry_bytes() const { return fi_learner_entry_bytes(handles_[0]); }
+    size_t players() const { return handles_.size(); }
+    const fi_step_stats& last_stats(size_t p) const { return stats_.at(p); }
+    std::string last_error(size_t p = 0) const {
+        std::lock_guard<std::mutex> g(mu_);
+        return err_.at(p);
+    }
+    fi_learner* handle(size_t p) { return handles_.at(p); }
+    const LearnerConfig& config() const { return cfg_; }
+
+private:
+    bool fail(size_t p, const std::string& m) {
+        std::lock_guard<std::mutex> g(mu_);
+        err_.at(p < err_.size() ? p : 0) = m;
+        return false;
+    }
+    void release() {
+        for (auto& h : handles_) {
+            if (h) fi_learner_destroy(h);
+            h = nullptr;
+        }
+    }
+
+    LearnerConfig cfg_;
+    std::vector<fi_learner*> handles_;
+    std::vector<fi_step_stats> stats_;
+    mutable std::mutex mu_;
+    std::vector<std::string> err_;
+};
+
+}  // namespace freeimpala_amd

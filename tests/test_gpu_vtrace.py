@@ -42,6 +42,7 @@ def run_vtrace(pi, mu, act, rew, disc, val, variant=0, **hp):
     loss = hip.DeviceBuffer(3 * 8)
     wsb = _abi.lib().fi_vtrace_workspace_bytes(T, B, A)
     ws = hip.DeviceBuffer(wsb)
+    ws.zero()
     rc = _abi.lib().fi_vtrace_loss_fp32_variant(
         variant, T, B, A, bufs["pi"].ptr, bufs["mu"].ptr, bufs["act"].ptr, bufs["rew"].ptr,
         bufs["disc"].ptr, bufs["val"].ptr, C.byref(H), vs.ptr, adv.ptr, dl.ptr, dv.ptr, loss.ptr,
