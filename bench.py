@@ -151,21 +151,17 @@ def main():
     if ws > 1:
         dist.init_process_group("gloo", rank=rank, world_size=ws)
 
+    from freeimpala_amd.launch import broadcast_bytes, max_over_ranks, shard_columns
     from freeimpala_amd.learner import DeviceLearner
 
     T, B, A = args.seq_len, args.batch, args.num_actions
     L = DeviceLearner(args.arch, seq_len=T, batch=B, num_actions=A, device=local,
                       optimizer="adam", publish="bf16" if args.arch == "atari" else "fp32")
-    L.synth(seed=42, b_global=B * N, b_offset=rank * B)
+    b_off, _ = shard_columns(rank, N, B)
+    L.synth(seed=42, b_global=B * N, b_offset=b_off)
     if ws > 1:  # RCCL communicator for the in-step gradient all-reduce (uid via gloo)
-        blob = DeviceLearner.comm_unique_id() if rank == 0 else b""
-        size = torch.tensor([len(blob)], dtype=torch.int64)
-        dist.broadcast(size, 0)
-        uid = torch.zeros(int(size.item()), dtype=torch.uint8)
-        if rank == 0:
-            uid[:] = torch.frombuffer(bytearray(blob), dtype=torch.uint8)
-        dist.broadcast(uid, 0)
-        L.attach_comm(uid.numpy().tobytes(), rank, ws)
+        uid = broadcast_bytes(DeviceLearner.comm_unique_id() if rank == 0 else b"", 0)
+        L.attach_comm(uid, rank, ws)
 
     def barrier():
         L.sync()
@@ -182,9 +178,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     if ws > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = max_over_ranks(elapsed)
     ms_per_step = 1000.0 * elapsed / args.steps
     value = T * B * N * args.steps / elapsed
 

@@ -10,7 +10,7 @@
 //     `batch` that SharedBuffer::readBatch returns (data_structures.h:267-300):
 //     M entries of S * ELEMENT_SIZE bytes, record schema in DESIGN.md section 3.
 //   * DeviceLearner::publish(player_index, blob, version) -- the bytes and version that go
-//     into Model::update / ModelManager::updateModel (data_structures.h:134-140, 441-451);
+//     into Model::update / ModelManager::updateModel (data_structures.h:141-148, 441-451);
 //     blob size == param_bytes() is the ModelManager model_size.
 // One fi_learner handle per player (the reference runs one worker thread per player,
 // learner.h:158-163): handles own their HIP stream and device memory, so different
