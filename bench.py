@@ -193,6 +193,13 @@ def main():
     st = L.step_resident(stats=True)
 
     work = kernel_work(args.arch, T, B, A)
+    # HBM bytes per launch from the committed rocprofv3 PMC passes (scripts/pmc_pass.sh,
+    # corrected as MI355X_MICROARCH.md prescribes); only valid for the same T/B/A config
+    traffic = {}
+    tpath = os.path.join(ROOT, "profiles", f"r01_pmc_traffic_{args.arch}.json")
+    if os.path.exists(tpath) and (T, B, A) == (100, 4096, 18):
+        with open(tpath) as fh:
+            traffic = {k: v["hbm_bytes_per_launch"] for k, v in json.load(fh).items() if not k.startswith("_")}
     per_step = {k: v["ms"] * v["count"] / max(1, args.profile_steps) for k, v in kt.items()}
     dominant = max(per_step, key=per_step.get) if per_step else None
     dtype = "bf16" if args.arch == "atari" else "fp32"
@@ -202,15 +209,17 @@ def main():
             return None
         kind, amount = work[name]
         ms = kt[name]["ms"] if ms is None else ms
+        tr = traffic.get(name)
         if kind == "byte":
             ach = amount / (ms * 1e-3) / 1e9
             return {"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": tr,
                     "algorithmic_per_launch": amount, "launch_ms": round(ms, 5)}
         ach = amount / (ms * 1e-3) / 1e12
         peak = MFMA_PEAK_TFLOPS[dtype]
         return {"kernel": name, "bound": "mfma", "achieved": round(ach, 2), "peak": peak,
-                "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": None,
+                "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": tr,
+                "traffic_unit": "HBM bytes per launch (rocprofv3 PMC)" if tr else None,
                 "algorithmic_per_launch": amount, "launch_ms": round(ms, 5)}
 
     result = {

@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libfi_learner.so")
+LIB_PATH = os.environ.get("FI_LIB_OVERRIDE") or os.path.join(_HERE, "lib", "libfi_learner.so")  # override: A/B experiment builds only
 
 FI_OK = 0
 FI_ARCH_MLP, FI_ARCH_ATARI = 0, 1

@@ -117,7 +117,7 @@ __global__ __launch_bounds__(256, 1) void conv1_fwd_fr(const uint8_t* __restrict
 #pragma unroll
         for (int i = 0; i < c1::OUT_PER_T; ++i) {
             const int c = threadIdx.x + 256 * i;
-            if (c < c1::OUT_CH) __builtin_nontemporal_store(((const u32x4*)out)[c], dst + c);
+            if (c < c1::OUT_CH) FI_ST16(((const u32x4*)out)[c], dst + c);
         }
     }
 }
@@ -425,7 +425,7 @@ __global__ __launch_bounds__(256, 1) void conv2_bwd_fr(const __bf16* __restrict_
                     bf16x8 o;
 #pragma unroll
                     for (int j = 0; j < 8; ++j) o[j] = (float)m[j] > 0.f ? v[j] : (__bf16)0.f;
-                    __builtin_nontemporal_store(__builtin_bit_cast(u32x4, o), dst + P);
+                    FI_ST16(__builtin_bit_cast(u32x4, o), dst + P);
                 }
             }
             issued += STORES;  // (wave 0 issues one more; counting fewer only waits longer)
@@ -635,7 +635,7 @@ __global__ __launch_bounds__(256, 1) void conv3_bwd_fr(const __bf16* __restrict_
                     bf16x8 o;
 #pragma unroll
                     for (int j = 0; j < 8; ++j) o[j] = (float)m[j] > 0.f ? v[j] : (__bf16)0.f;
-                    __builtin_nontemporal_store(__builtin_bit_cast(u32x4, o), dst + P);
+                    FI_ST16(__builtin_bit_cast(u32x4, o), dst + P);
                 }
             }
             issued += STORES;

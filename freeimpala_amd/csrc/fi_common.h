@@ -77,6 +77,13 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_base) {
         : "memory");
 }
 
+// Streaming 16-byte store of an output tile (nontemporal unless FI_PLAIN_STORES: A/B knob).
+#ifdef FI_PLAIN_STORES
+#define FI_ST16(v, p) (*(p) = (v))
+#else
+#define FI_ST16(v, p) __builtin_nontemporal_store((v), (p))
+#endif
+
 // Raw buffer descriptor (stride 0, range-checked to `bytes`) from wave-uniform inputs.
 typedef int fi_i32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ fi_i32x4 make_rsrc(const void* base, uint32_t bytes) {
