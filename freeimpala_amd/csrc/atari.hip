@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "atari.h"
+#include "fc_blaslt.h"
 #include "fi_common.h"
 #include "kernels.h"
 
@@ -466,6 +467,61 @@ static int wgrad(LA la, LB lb, float* slab, float* cs_slab, int M, int I, int J,
     return FI_OK;
 }
 
+// ------------------------------------------------------------------ small bf16 helpers
+// column sums of a row-major bf16 [M][C] tensor (C % 8 == 0, C <= 2048) into fp32 slabs
+// [kColsumSplits][C] (reduced in a fixed order by reduce_slabs: deterministic)
+constexpr int kColsumSplits = 512;
+__global__ __launch_bounds__(256) void colsum_bf16_kernel(const __bf16* __restrict__ Y, int M, int C,
+                                                         float* __restrict__ slab) {
+    __shared__ float red[2048];
+    const int tpr = C / 8;                     // threads per row
+    const int rpi = 256 / tpr;                 // rows per iteration
+    const int lr = threadIdx.x / tpr, c8 = threadIdx.x % tpr;
+    const int rows_per = (M + gridDim.x - 1) / gridDim.x;
+    const int r0 = blockIdx.x * rows_per, r1 = min(M, r0 + rows_per);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (lr < rpi)
+        for (int r = r0 + lr; r < r1; r += rpi) {
+            const bf16x8 v = *(const bf16x8*)(Y + (size_t)r * C + 8 * c8);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[j] += (float)v[j];
+        }
+    for (int i = threadIdx.x; i < C; i += 256) red[i] = 0.f;
+    __syncthreads();
+    for (int g = 0; g < rpi; ++g) {  // fixed order over the row groups
+        if (lr == g)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) red[8 * c8 + j] += acc[j];
+        __syncthreads();
+    }
+    for (int i = threadIdx.x; i < C; i += 256) slab[(size_t)blockIdx.x * C + i] = red[i];
+}
+
+static int colsum_bf16(const __bf16* Y, int M, int C, float* slab, hipStream_t s) {
+    FI_REQUIRE(C % 8 == 0 && C / 8 <= 256 && C <= 2048, "colsum_bf16: bad width");
+    hipLaunchKernelGGL(colsum_bf16_kernel, dim3(kColsumSplits), dim3(256), 0, s, Y, M, C, slab);
+    FI_HIP_CHECK(hipGetLastError());
+    return FI_OK;
+}
+
+// y *= (m > 0) elementwise (generic path only; the frame-resident conv3 backward masks in LDS)
+__global__ void relu_mask_bf16_kernel(__bf16* __restrict__ y, const __bf16* __restrict__ m, size_t n8) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n8; i += (size_t)gridDim.x * blockDim.x) {
+        bf16x8 v = ((bf16x8*)y)[i];
+        const bf16x8 k = ((const bf16x8*)m)[i];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (float)k[j] > 0.f ? v[j] : (__bf16)0.f;
+        ((bf16x8*)y)[i] = v;
+    }
+}
+
+static int relu_mask_bf16(__bf16* y, const __bf16* m, size_t n, hipStream_t s) {
+    FI_REQUIRE(n % 8 == 0, "relu_mask_bf16: n % 8");
+    hipLaunchKernelGGL(relu_mask_bf16_kernel, dim3(2048), dim3(256), 0, s, y, m, n / 8);
+    FI_HIP_CHECK(hipGetLastError());
+    return FI_OK;
+}
+
 // ------------------------------------------------------------------ weight layouts (bf16)
 struct WeightsBf16 {
     __bf16 *c1T, *c2T, *c3T, *fcT, *hT;  // forward B operands [out][k]
@@ -524,6 +580,7 @@ struct AtariImpl {
     std::vector<void*> allocs;
     int cs2 = 0, cs3 = 0;  // class strides for the dgrad GEMMs
     bool fr = true;        // frame-resident kernels (FI_ATARI_GENERIC=1 -> generic GEMMs)
+    FcBlasLt* fc = nullptr;  // fc layer GEMMs (hipBLASLt)
 };
 
 int conv1_fwd_fr_launch(const uint8_t* frames, const __bf16* w1t, const float* bias, __bf16* a1,
@@ -532,8 +589,8 @@ int conv1_wgrad_fr_launch(const uint8_t* frames, const __bf16* da1, float* slab,
                           int nframes, int grid, hipStream_t s);
 int conv2_bwd_fr_launch(const __bf16* a1, const __bf16* da2, const __bf16* w2d, __bf16* da1, float* slab,
                         float* cs_slab, int nframes, int grid, hipStream_t s);
-int conv3_bwd_fr_launch(const __bf16* a2, const __bf16* da3, const __bf16* w3d, __bf16* da2, float* slab,
-                        float* cs_slab, int nframes, int grid, hipStream_t s);
+int conv3_bwd_fr_launch(const __bf16* a2, const __bf16* da3, const __bf16* a3, const __bf16* w3d, __bf16* da2,
+                        float* slab, float* cs_slab, int nframes, int grid, hipStream_t s);
 constexpr int FR_GRID = 256;  // persistent frame-resident workgroups (1 per CU)
 
 static AtariImpl* impl(AtariNet* n) { return (AtariImpl*)n->impl; }
@@ -585,6 +642,18 @@ AtariNet* atari_create(int B, int T, int A) {
         atari_destroy(n);
         return nullptr;
     }
+    hipStream_t s0;
+    if (hipStreamCreate(&s0) != hipSuccess) {
+        set_error("atari: hipStreamCreate failed");
+        atari_destroy(n);
+        return nullptr;
+    }
+    I->fc = fc_blaslt_create((int)N, I->a3, I->wb.fcB, I->dh, I->h, I->da3, I->slab, s0);
+    (void)hipStreamDestroy(s0);
+    if (!I->fc) {  // fc_blaslt_create set the error
+        atari_destroy(n);
+        return nullptr;
+    }
     return n;
 }
 
@@ -592,6 +661,7 @@ void atari_destroy(AtariNet* n) {
     if (!n) return;
     AtariImpl* I = impl(n);
     if (I) {
+        fc_blaslt_destroy(I->fc);
         for (void* p : I->allocs) (void)hipFree(p);
         delete I;
     }
@@ -627,8 +697,7 @@ int atari_forward(AtariNet* n, const uint8_t* frames, float* logits, float* valu
     { TagScope ts(tg, "conv3_fwd"); rc = gemm<128, 64, 2, 2>(ConvGather<9, 64, 3, 1, 7>{I->a2, N * P3}, RowsBf16{I->wb.c3T, C3O, C3K},
                              EpiAct{I->a3, C3O, p + o.c3b, 1.0f}, N * P3, C3O, C3K, s); }
     if (rc) return rc;
-    { TagScope ts(tg, "fc_fwd"); rc = gemm<128, 128, 2, 2>(RowsBf16{I->a3, N, FCK}, RowsBf16{I->wb.fcT, FCO, FCK},
-                              EpiAct{I->h, FCO, p + o.fcb, 1.0f}, N, FCO, FCK, s); }
+    { TagScope ts(tg, "fc_fwd"); rc = fc_blaslt_forward(I->fc, I->a3, I->wb.fcB, p + o.fcb, I->h, s); }
     if (rc) return rc;
     { TagScope ts(tg, "heads_fwd"); rc = gemm<128, 32, 4, 1>(RowsBf16{I->h, N, FCO}, RowsBf16{I->wb.hT, HP, FCO},
                              EpiHeadsOut{logits, values, p + o.hb, I->A}, N, HP, FCO, s); }
@@ -653,19 +722,20 @@ int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, con
     FI_A("heads_dgrad", (gemm<128, 128, 2, 2>(dout, RowsBf16{I->wb.hD, FCO, HP}, EpiMaskBf16{I->dh, I->h, FCO}, N, FCO,
                                HP, s)));
     // fc: wgrad [3136][512] + bias, dgrad -> da3 (masked by a3)
-    FI_A("fc_wgrad", (wgrad<128, 128, 2, 2>(RowsBf16{I->a3, N, FCK}, RowsBf16{I->dh, N, FCO}, slab, cs, N, FCK, FCO,
-                                SPL_FC, 1.f, s)));
-    FI_A("reduce_slabs", reduce_slabs(slab, SPL_FC, (size_t)FCK * FCO, grads + o.fcw, s));
-    FI_A("reduce_slabs", reduce_slabs(cs, SPL_FC, (size_t)FCO, grads + o.fcb, s));
-    FI_A("fc_dgrad", (gemm<128, 128, 2, 2>(RowsBf16{I->dh, N, FCO}, RowsBf16{I->wb.fcB, FCK, FCO},
-                               EpiMaskBf16{I->da3, I->a3, FCK}, N, FCK, FCO, s)));
+    // fc (hipBLASLt): wgrad straight into the gradient blob, bias = column sums of dh,
+    // dgrad -> da3 unmasked (conv3's backward applies the a3 ReLU mask as it loads da3)
+    FI_A("fc_wgrad", fc_blaslt_wgrad(I->fc, I->a3, I->dh, grads + o.fcw, s));
+    FI_A("fc_bias", colsum_bf16(I->dh, N, FCO, slab, s));
+    FI_A("reduce_slabs", reduce_slabs(slab, kColsumSplits, (size_t)FCO, grads + o.fcb, s));
+    FI_A("fc_dgrad", fc_blaslt_dgrad(I->fc, I->dh, I->wb.fcB, I->da3, s));
     // conv3: wgrad [576][64] + bias, dgrad -> da2 (masked by a2)
     if (I->fr) {
         const int grid = std::min(N, FR_GRID);
-        FI_A("conv3_bwd", conv3_bwd_fr_launch(I->a2, I->da3, I->wb.c3D, I->da2, slab, cs, N, grid, s));
+        FI_A("conv3_bwd", conv3_bwd_fr_launch(I->a2, I->da3, I->a3, I->wb.c3D, I->da2, slab, cs, N, grid, s));
         FI_A("reduce_slabs", reduce_slabs(slab, grid, (size_t)C3K * C3O, grads + o.c3w, s));
         FI_A("reduce_slabs", reduce_slabs(cs, grid, (size_t)C3O, grads + o.c3b, s));
     } else {
+        FI_A("relu_mask", relu_mask_bf16(I->da3, I->a3, (size_t)N * FCK, s));
         FI_A("conv3_wgrad", (wgrad<128, 64, 2, 2>(ConvGather<9, 64, 3, 1, 7>{I->a2, N * P3}, RowsBf16{I->da3, N * P3, C3O},
                                    slab, cs, N * P3, C3K, C3O, SPL_C3, 1.f, s)));
         FI_A("reduce_slabs", reduce_slabs(slab, SPL_C3, (size_t)C3K * C3O, grads + o.c3w, s));

@@ -479,9 +479,10 @@ int conv2_bwd_fr_launch(const __bf16* a1, const __bf16* da2, const __bf16* w2d, 
 namespace c3 {
 constexpr int XB = 11 * 1024;                // 81 px * 128 B = 10,368, padded to 11 KiB
 constexpr int DYB = 18 * 1024;               // 11x11 bordered rows * 144 B = 17,424
-constexpr int SLOT = XB + DYB;               // 29,696
+constexpr int MB = 7 * 1024;                 // a3 tile (ReLU mask of dY): 49 px * 128 B = 6,272
+constexpr int SLOT = XB + DYB + MB;          // 36,864
 constexpr int RING = 3;
-constexpr int NX = 11, NDY = 18;  // 11 + 18 pieces
+constexpr int NX = 11, NDY = 18, NM = 7;     // 11 + 18 + 7 pieces
 constexpr int OUTT = 81 * 128;               // dgrad tile [81][64] bf16
 constexpr int OUT_CH = 81 * 8;               // 648
 }  // namespace c3
@@ -489,11 +490,16 @@ constexpr int OUT_CH = 81 * 8;               // 648
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// wave w DMAs X pieces j = w + 4i (< 11; lanes past pixel 81 read zeros) and dY pieces
-// d = w + 4k (< 18)
-__device__ __forceinline__ void c3_issue(const __bf16* x, const __bf16* dy, const uint32_t (&dvo)[5],
-                                         uint32_t slot_lds, int w, int lane) {
-    const fi_i32x4 xr = make_rsrc(x, 10368), dr = make_rsrc(dy, 6272);
+// wave w DMAs X pieces j = w + 4i (< 11; lanes past pixel 81 read zeros), dY pieces
+// d = w + 4k (< 18) and a3 (mask) pieces m = w + 4k (< 7)
+__device__ __forceinline__ void c3_issue(const __bf16* x, const __bf16* dy, const __bf16* a3,
+                                         const uint32_t (&dvo)[5], uint32_t slot_lds, int w, int lane) {
+    const fi_i32x4 xr = make_rsrc(x, 10368), dr = make_rsrc(dy, 6272), mr = make_rsrc(a3, 6272);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int m = w + 4 * k;
+        if (k < 1 || m < c3::NM) blds16(mr, 16 * lane + 1024 * m, slot_lds + c3::XB + c3::DYB + m * 1024);
+    }
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         const int j = w + 4 * i;
@@ -507,7 +513,8 @@ __device__ __forceinline__ void c3_issue(const __bf16* x, const __bf16* dy, cons
 }
 
 __global__ __launch_bounds__(256, 1) void conv3_bwd_fr(const __bf16* __restrict__ a2,
-                                                       const __bf16* __restrict__ da3,
+                                                       const __bf16* __restrict__ da3,  // unmasked
+                                                       const __bf16* __restrict__ a3,   // its mask
                                                        const __bf16* __restrict__ w3d,  // [64 ci][576]
                                                        __bf16* __restrict__ da2,
                                                        float* __restrict__ slab,     // [grid][576][64]
@@ -560,13 +567,14 @@ __global__ __launch_bounds__(256, 1) void conv3_bwd_fr(const __bf16* __restrict_
     for (int i = 0; i < 5; ++i) { accw[i][0] = f32x16{}; accw[i][1] = f32x16{}; }
     float bsum0 = 0.f, bsum1 = 0.f;
 
-    const int npw = (c3::NX - w + 3) / 4 + (c3::NDY - w + 3) / 4;
+    const int npw = (c3::NX - w + 3) / 4 + (c3::NDY - w + 3) / 4 + (c3::NM - w + 3) / 4;
     constexpr int STORES = c3::OUT_CH / 256;  // 2
     int issued = 0, m0 = 0, m1 = 0, m2 = 0;
     const int nmine = nframes > (int)blockIdx.x ? (nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
     for (int i = 0; i < 3 && i < nmine; ++i) {
         const int f = blockIdx.x + i * gridDim.x;
-        c3_issue(a2 + (size_t)f * 5184, da3 + (size_t)f * 3136, dvo, lds0 + i * c3::SLOT, w, lane);
+        c3_issue(a2 + (size_t)f * 5184, da3 + (size_t)f * 3136, a3 + (size_t)f * 3136, dvo, lds0 + i * c3::SLOT, w,
+                 lane);
         issued += npw;
         if (i == 0) m0 = issued; else if (i == 1) m1 = issued; else m2 = issued;
     }
@@ -575,6 +583,21 @@ __global__ __launch_bounds__(256, 1) void conv3_bwd_fr(const __bf16* __restrict_
         const int slot = it % 3;
         char* X = smem + slot * c3::SLOT;
         wait_vmcnt(issued - m0);
+        lds_barrier();
+        // ReLU mask of the upstream gradient: dY *= (a3 > 0), 49 px x 8 chunks of 16 B
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int qq = threadIdx.x + 256 * i;
+            if (qq < 392) {
+                const int p = qq >> 3, c = qq & 7, py = p / 7, px = p - 7 * py;
+                bf16x8* dyp = (bf16x8*)(X + c3::XB + DP * ((py + 2) * 11 + px + 2) + 16 * c);
+                const bf16x8 m = *(const bf16x8*)(X + c3::XB + c3::DYB + 128 * p + 16 * c);
+                bf16x8 v = *dyp;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = (float)m[j] > 0.f ? v[j] : (__bf16)0.f;
+                *dyp = v;
+            }
+        }
         lds_barrier();
 
         // ---------------- weight gradient
@@ -644,7 +667,8 @@ __global__ __launch_bounds__(256, 1) void conv3_bwd_fr(const __bf16* __restrict_
         int m3 = 0;
         if (it + 3 < nmine) {
             const int fn = blockIdx.x + (it + 3) * gridDim.x;
-            c3_issue(a2 + (size_t)fn * 5184, da3 + (size_t)fn * 3136, dvo, lds0 + slot * c3::SLOT, w, lane);
+            c3_issue(a2 + (size_t)fn * 5184, da3 + (size_t)fn * 3136, a3 + (size_t)fn * 3136, dvo,
+                     lds0 + slot * c3::SLOT, w, lane);
             issued += npw;
             m3 = issued;
         }
@@ -676,9 +700,9 @@ __global__ __launch_bounds__(256, 1) void conv3_bwd_fr(const __bf16* __restrict_
     }
 }
 
-int conv3_bwd_fr_launch(const __bf16* a2, const __bf16* da3, const __bf16* w3d, __bf16* da2, float* slab,
-                        float* cs_slab, int nframes, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(conv3_bwd_fr, dim3(grid), dim3(256), 0, s, a2, da3, w3d, da2,
+int conv3_bwd_fr_launch(const __bf16* a2, const __bf16* da3, const __bf16* a3, const __bf16* w3d, __bf16* da2,
+                        float* slab, float* cs_slab, int nframes, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(conv3_bwd_fr, dim3(grid), dim3(256), 0, s, a2, da3, a3, w3d, da2,
                        slab, cs_slab, nframes);
     FI_HIP_CHECK(hipGetLastError());
     return FI_OK;

@@ -1,0 +1,168 @@
+// fc_blaslt.cpp -- the Atari policy's fully connected layer (3136 -> 512) on hipBLASLt.
+//
+// The fc layer is three plain bf16 GEMMs over R = (T+1)*B rows (no gathers, no fused
+// masks of other tensors), which is what the library GEMM is for (hand-written MFMA kernels
+// stay on the convolutions, the heads and the V-trace scan):
+//   forward  h[R][512]    = relu(a3[R][3136] W[3136][512] + b)   (epilogue RELU_BIAS, bf16 out)
+//   dgrad    da3[R][3136] = dh[R][512] W^T                      (bf16 out; the ReLU mask of
+//                                                                 a3 is applied where conv3's
+//                                                                 backward reads da3)
+//   wgrad    dW[3136][512] = a3^T dh  (fp32 out, straight into the gradient blob)
+// All row-major; hipBLASLt is column-major, so each call computes the transposed product.
+// W is the bf16 copy of the fp32 master in the oracle's [3136][512] order.
+// Algorithms: the heuristic's top candidates are timed once at creation and the fastest kept.
+#include <hip/hip_runtime.h>
+#include <hipblaslt/hipblaslt.h>
+
+#include <string>
+
+#include "fc_blaslt.h"
+#include "fi_common.h"
+
+namespace fi {
+
+struct FcGemm {
+    hipblasLtMatmulDesc_t desc = nullptr;
+    hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, ld = nullptr;
+    hipblasLtMatmulAlgo_t algo{};
+};
+
+struct FcBlasLt {
+    hipblasLtHandle_t h = nullptr;
+    void* ws = nullptr;
+    size_t wsb = 0;
+    FcGemm g[3];  // 0 forward, 1 dgrad, 2 wgrad
+    int rows = 0;
+};
+
+static std::string blt_err(const char* what, int st) { return std::string(what) + " failed: hipblasStatus " + std::to_string(st); }
+#define BLT(x)                                                            \
+    do {                                                                  \
+        const int st_ = (int)(x);                                         \
+        if (st_ != 0) { set_error(blt_err(#x, st_)); return FI_ERR_HIP; } \
+    } while (0)
+
+static int make_gemm(FcBlasLt* F, FcGemm& G, int m, int n, int k, bool ta, bool tb, hipDataType dt_d,
+                     hipblasLtEpilogue_t epi, const void* A, const void* B, void* D, hipStream_t s) {
+    BLT(hipblasLtMatmulDescCreate(&G.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F));
+    const hipblasOperation_t opa = ta ? HIPBLAS_OP_T : HIPBLAS_OP_N, opb = tb ? HIPBLAS_OP_T : HIPBLAS_OP_N;
+    BLT(hipblasLtMatmulDescSetAttribute(G.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &opa, sizeof(opa)));
+    BLT(hipblasLtMatmulDescSetAttribute(G.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &opb, sizeof(opb)));
+    BLT(hipblasLtMatmulDescSetAttribute(G.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &epi, sizeof(epi)));
+    if (epi == HIPBLASLT_EPILOGUE_RELU_BIAS) {
+        const hipDataType bt = HIP_R_32F;
+        BLT(hipblasLtMatmulDescSetAttribute(G.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt)));
+    }
+    BLT(hipblasLtMatrixLayoutCreate(&G.la, HIP_R_16BF, ta ? k : m, ta ? m : k, ta ? k : m));
+    BLT(hipblasLtMatrixLayoutCreate(&G.lb, HIP_R_16BF, tb ? n : k, tb ? k : n, tb ? n : k));
+    BLT(hipblasLtMatrixLayoutCreate(&G.ld, dt_d, m, n, m));
+    hipblasLtMatmulPreference_t pref;
+    BLT(hipblasLtMatmulPreferenceCreate(&pref));
+    BLT(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &F->wsb,
+                                              sizeof(F->wsb)));
+    hipblasLtMatmulHeuristicResult_t res[6];
+    int got = 0;
+    const int st = (int)hipblasLtMatmulAlgoGetHeuristic(F->h, G.desc, G.la, G.lb, G.ld, G.ld, pref, 6, res, &got);
+    hipblasLtMatmulPreferenceDestroy(pref);
+    if (st != 0 || got == 0) {
+        set_error("hipBLASLt: no algorithm for the fc GEMM (m=" + std::to_string(m) + " n=" + std::to_string(n) +
+                  " k=" + std::to_string(k) + ")");
+        return FI_ERR_UNSUPPORTED;
+    }
+    // time the candidates once (the tensors hold garbage at creation; only speed matters)
+    const float alpha = 1.f, beta = 0.f;
+    hipEvent_t e0, e1;
+    FI_HIP_CHECK(hipEventCreate(&e0));
+    FI_HIP_CHECK(hipEventCreate(&e1));
+    float best = 1e30f;
+    int bi = 0;
+    const void* bias = nullptr;
+    for (int a = 0; a < got; ++a) {
+        if (epi == HIPBLASLT_EPILOGUE_RELU_BIAS) {
+            bias = D;  // any readable device buffer of >= m floats
+            BLT(hipblasLtMatmulDescSetAttribute(G.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias)));
+        }
+        if (hipblasLtMatmul(F->h, G.desc, &alpha, A, G.la, B, G.lb, &beta, D, G.ld, D, G.ld, &res[a].algo, F->ws,
+                            F->wsb, s) != 0)
+            continue;
+        FI_HIP_CHECK(hipEventRecord(e0, s));
+        for (int i = 0; i < 2; ++i)
+            BLT(hipblasLtMatmul(F->h, G.desc, &alpha, A, G.la, B, G.lb, &beta, D, G.ld, D, G.ld, &res[a].algo,
+                                F->ws, F->wsb, s));
+        FI_HIP_CHECK(hipEventRecord(e1, s));
+        FI_HIP_CHECK(hipEventSynchronize(e1));
+        float ms = 0.f;
+        FI_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+        if (ms < best) { best = ms; bi = a; }
+    }
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    if (best >= 1e30f) {
+        set_error("hipBLASLt: every fc GEMM candidate failed to launch");
+        return FI_ERR_UNSUPPORTED;
+    }
+    G.algo = res[bi].algo;
+    return FI_OK;
+}
+
+FcBlasLt* fc_blaslt_create(int rows, const void* a3, const void* w, const void* dh, void* h, void* da3,
+                           float* dw, hipStream_t s) {
+    FcBlasLt* F = new FcBlasLt();
+    F->rows = rows;
+    F->wsb = 64u << 20;
+    int rc = FI_OK;
+    if (hipblasLtCreate(&F->h) != 0) {
+        set_error("hipblasLtCreate failed");
+        rc = FI_ERR_HIP;
+    }
+    if (rc == FI_OK && hipMalloc(&F->ws, F->wsb) != hipSuccess) {
+        set_error("hipBLASLt workspace allocation failed");
+        rc = FI_ERR_OOM;
+    }
+    constexpr int K = 3136, N = 512;
+    // column-major views of the row-major products (see the header comment)
+    if (rc == FI_OK) rc = make_gemm(F, F->g[0], N, rows, K, false, false, HIP_R_16BF, HIPBLASLT_EPILOGUE_RELU_BIAS, w, a3, h, s);
+    if (rc == FI_OK) rc = make_gemm(F, F->g[1], K, rows, N, true, false, HIP_R_16BF, HIPBLASLT_EPILOGUE_DEFAULT, w, dh, da3, s);
+    if (rc == FI_OK) rc = make_gemm(F, F->g[2], N, K, rows, false, true, HIP_R_32F, HIPBLASLT_EPILOGUE_DEFAULT, dh, a3, dw, s);
+    if (rc == FI_OK && hipStreamSynchronize(s) != hipSuccess) rc = FI_ERR_HIP;
+    if (rc != FI_OK) {
+        fc_blaslt_destroy(F);
+        return nullptr;
+    }
+    return F;
+}
+
+void fc_blaslt_destroy(FcBlasLt* F) {
+    if (!F) return;
+    for (auto& G : F->g) {
+        if (G.la) hipblasLtMatrixLayoutDestroy(G.la);
+        if (G.lb) hipblasLtMatrixLayoutDestroy(G.lb);
+        if (G.ld) hipblasLtMatrixLayoutDestroy(G.ld);
+        if (G.desc) hipblasLtMatmulDescDestroy(G.desc);
+    }
+    if (F->ws) (void)hipFree(F->ws);
+    if (F->h) hipblasLtDestroy(F->h);
+    delete F;
+}
+
+static int run(FcBlasLt* F, FcGemm& G, const void* A, const void* B, void* D, hipStream_t s) {
+    const float alpha = 1.f, beta = 0.f;
+    BLT(hipblasLtMatmul(F->h, G.desc, &alpha, A, G.la, B, G.lb, &beta, D, G.ld, D, G.ld, &G.algo, F->ws, F->wsb, s));
+    return FI_OK;
+}
+
+int fc_blaslt_forward(FcBlasLt* F, const void* a3, const void* w, const float* bias, void* h, hipStream_t s) {
+    const void* b = bias;
+    BLT(hipblasLtMatmulDescSetAttribute(F->g[0].desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &b, sizeof(b)));
+    return run(F, F->g[0], w, a3, h, s);
+}
+
+int fc_blaslt_dgrad(FcBlasLt* F, const void* dh, const void* w, void* da3, hipStream_t s) {
+    return run(F, F->g[1], w, dh, da3, s);
+}
+
+int fc_blaslt_wgrad(FcBlasLt* F, const void* a3, const void* dh, float* dw, hipStream_t s) {
+    return run(F, F->g[2], dh, a3, dw, s);
+}
+
+}  // namespace fi
