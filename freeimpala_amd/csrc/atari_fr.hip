@@ -27,7 +27,40 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+#ifdef FI_STAMPS  // timing experiment: wave-0 s_memrealtime stamps per workgroup, printed by the launcher
+__device__ unsigned long long fi_stamps[256 * 32];
+#define ST_DECL unsigned long long st_[32]; int sn_ = 0;
+#define ST() do { if (sn_ < 32) st_[sn_++] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define ST_FLUSH() do { if (threadIdx.x == 0 && blockIdx.x < 256) for (int i_ = 0; i_ < 32; ++i_) fi_stamps[blockIdx.x * 32 + i_] = i_ < sn_ ? st_[i_] : 0ull; } while (0)
+#include <cstdio>
+#include <vector>
+#include <algorithm>
+static void st_report(const char* name) {
+    static int calls = 0;
+    if (++calls != 4) return;
+    (void)hipDeviceSynchronize();
+    std::vector<unsigned long long> h(256 * 32);
+    (void)hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(fi_stamps), h.size() * 8);
+    unsigned long long t0 = ~0ull;
+    for (int b = 0; b < 256; ++b) t0 = std::min(t0, h[b * 32]);
+    std::fprintf(stderr, "[stamps %s] us rel. to first start: idx: min/med/max\n", name);
+    for (int i = 0; i < 32; ++i) {
+        std::vector<double> v;
+        for (int b = 0; b < 256; ++b) if (h[b * 32 + i]) v.push_back((h[b * 32 + i] - t0) * 0.01);
+        if (v.empty()) break;
+        std::sort(v.begin(), v.end());
+        std::fprintf(stderr, "  %2d: %8.2f %8.2f %8.2f\n", i, v.front(), v[v.size() / 2], v.back());
+    }
+}
+#else
+#define ST_DECL
+#define ST() do {} while (0)
+#define ST_FLUSH() do {} while (0)
+static void st_report(const char*) {}
+#endif
 
 namespace c1 {
 constexpr int FRAME_LOADS = 84 * 84 * 4 / 16;       // 1764 16-byte loads per frame
@@ -70,56 +103,126 @@ __device__ __forceinline__ void c1_store_image(char* img, const u32x4 (&r)[c1::P
 }
 
 // ---------------------------------------------------------------------------------
-// conv1 forward: a1[f] = bf16(relu(conv(frames[f]) / 255 + b)), persistent over frames
+// conv1 forward: a1[f] = bf16(relu(conv(frames[f]) / 255 + b)), persistent over frames.
+// The raw u8 frames stream through a 2-slot LDS-DMA ring (two frames in flight while one is
+// computed); each frame is converted once into the bf16 pair-plane image.
 // ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(256, 1) void conv1_fwd_fr(const uint8_t* __restrict__ frames,
+namespace c1 {
+constexpr int RAW = 28 * 1024;          // one raw frame (28,224 B) in 28 1-KiB DMA pieces
+}
+
+// 8 waves: wave w DMAs raw pieces j = w + 8i (< 28)
+__device__ __forceinline__ int c1_issue_raw(const uint8_t* fr, uint32_t slot_lds, int w, int lane) {
+    const fi_i32x4 rr = make_rsrc(fr, 28224);  // bytes past the frame read as zeros
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int j = w + 8 * i;
+        if (i < 3 || j < 28) blds16(rr, 16 * lane + 1024 * j, slot_lds + 1024 * j);
+    }
+    return w < 4 ? 4 : 3;
+}
+
+// 512 threads = two waves per SIMD: one wave's LDS / DMA waits hide behind the other's MFMAs.
+// Wave w computes all 32 output channels of the pixel tiles w, w+8, w+16 (, w+24).
+__global__ __launch_bounds__(512, 2) void conv1_fwd_fr(const uint8_t* __restrict__ frames,
                                                        const __bf16* __restrict__ w1t,  // [32][256]
                                                        const float* __restrict__ bias,
                                                        __bf16* __restrict__ a1, int nframes) {
-    __shared__ __attribute__((aligned(16))) char smem[c1::IMG + c1::OUT];
-    char* img = smem;
-    __bf16* out = (__bf16*)(smem + c1::IMG);
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, h = lane >> 5, col = lane & 31;
-    // B fragments of all 16 K-steps stay in registers: lane holds W[n=col][k=16ks+8h..+8]
-    bf16x8 bw[16];
+    __shared__ __attribute__((aligned(16))) char smem[2 * c1::RAW + c1::IMG + c1::OUT];
+    char* img = smem + 2 * c1::RAW;
+    __bf16* out = (__bf16*)(smem + 2 * c1::RAW + c1::IMG);
+    const int lane = threadIdx.x & 63, w = wave_id();
+    const uint32_t lds0 = lds_addr(smem);
+    // 16x16x32 MFMAs with the weights as the A operand: D[channel][pixel], so a lane ends up
+    // with 4 consecutive channels of one pixel (one 8-byte LDS store). K-step ks = kernel row
+    // ky (32 k = 8 taps x 4 channels); W fragments of both channel halves stay in registers:
+    // lane holds W[c = 16nt + (lane&15)][k = 32ks + 8g..+8]
+    const int g = lane >> 4, c16 = lane & 15;
+    bf16x8 bw[2][8];
 #pragma unroll
-    for (int ks = 0; ks < 16; ++ks) bw[ks] = *(const bf16x8*)(w1t + col * 256 + ks * 16 + h * 8);
-    const float bcol = bias[col];
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks)
+            bw[nt][ks] = *(const bf16x8*)(w1t + (16 * nt + c16) * 256 + 32 * ks + 8 * g);
+    float bch[2][4];  // bias of the lane's output channels 16nt + 4g + r
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bch[nt][r] = bias[16 * nt + 4 * g + r];
     const float inv255 = 1.0f / 255.0f;
+    constexpr int ST_W = c1::OUT_CH / 512;  // 3 full store rounds (+1 for wave 0)
+    const int stores = ST_W + (w < (c1::OUT_CH - 512 * ST_W) / 64 ? 1 : 0);
 
-    u32x4 pre[c1::PER_T];
-    int f = blockIdx.x;
-    if (f < nframes) c1_fetch_frame(frames + (size_t)f * 28224, pre);
-    for (; f < nframes; f += gridDim.x) {
-        c1_store_image(img, pre);
-        const int fn = f + gridDim.x;
-        if (fn < nframes) c1_fetch_frame(frames + (size_t)fn * 28224, pre);
-        __syncthreads();  // image ready, previous out tile drained
-        // 13 row tiles of 32 output pixels: wave w takes tiles w, w+4, ...
-        for (int t = w; t < 13; t += 4) {
-            const int m = min(t * 32 + col, 399);
-            const int oy = m / 20, ox = m - oy * 20;
-            const char* abase = img + h * c1::PLANE + 16 * (oy * 4 * 21 + ox);
-            f32x16 acc = {};
+    const int nmine = nframes > (int)blockIdx.x ? (nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+    ST_DECL
+    ST();
+    int issued = 0, m0 = 0, m1 = 0;
+    if (nmine > 0) issued += c1_issue_raw(frames + (size_t)blockIdx.x * 28224, lds0, w, lane);
+    m0 = issued;
+    if (nmine > 1) issued += c1_issue_raw(frames + (size_t)(blockIdx.x + gridDim.x) * 28224, lds0 + c1::RAW, w, lane);
+    m1 = issued;
+    for (int it = 0; it < nmine; ++it) {
+        const int f = blockIdx.x + it * gridDim.x;
+        const char* raw = smem + (it & 1) * c1::RAW;
+        wait_vmcnt(issued - m0);
+        lds_barrier();  // raw frame landed; previous out tile drained, image free
+        if (it < 6) ST();
 #pragma unroll
-            for (int ks = 0; ks < 16; ++ks) {
-                const bf16x8 a = *(const bf16x8*)(abase + 16 * ((ks >> 1) * 21 + (ks & 1)));
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bw[ks], acc, 0, 0, 0);
-            }
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (row < 400) out[row * 32 + col] = (__bf16)fmaxf(acc[r] * inv255 + bcol, 0.f);
+        for (int i = 0; i < (c1::FRAME_LOADS + 511) / 512; ++i) {
+            const int u = threadIdx.x + 512 * i;
+            if (u < c1::FRAME_LOADS) {
+                bf16x8 lo, hi;
+                u8x16_to_bf16(*(const u32x4*)(raw + 16 * u), lo, hi);
+                *(bf16x8*)(img + 16 * u) = lo;
+                *(bf16x8*)(img + c1::PLANE + 16 * u) = hi;
             }
         }
-        __syncthreads();  // out tile complete, image free
+        lds_barrier();  // image ready; raw slot free
+        if (it < 6) ST();
+        int m2 = issued;
+        if (it + 2 < nmine) {
+            issued += c1_issue_raw(frames + (size_t)(f + 2 * gridDim.x) * 28224, lds0 + (it & 1) * c1::RAW, w, lane);
+            m2 = issued;
+        }
+        // 25 tiles of 16 output pixels; this wave: tiles w, w+8, ... (both channel halves)
+        for (int t = w; t < 25; t += 8) {
+            const int q = t * 16 + c16;
+            const int oy = q / 20, ox = q - 20 * oy;
+            // pixel pair (2ox + g) of input row 4oy + ky: plane g&1, slot (4oy+ky)*21 + ox + g/2
+            const char* ab = img + (g & 1) * c1::PLANE + 16 * (oy * 84 + ox + (g >> 1));
+            bf16x8 fa[8];
+#pragma unroll
+            for (int ks = 0; ks < 8; ++ks) fa[ks] = *(const bf16x8*)(ab + 16 * 21 * ks);
+            f32x4 d0 = {}, d1 = {};
+#pragma unroll
+            for (int ks = 0; ks < 8; ++ks) {
+                d0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[0][ks], fa[ks], d0, 0, 0, 0);
+                d1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[1][ks], fa[ks], d1, 0, 0, 0);
+            }
+            bf16x4 o0, o1;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                o0[r] = (__bf16)fmaxf(d0[r] * inv255 + bch[0][r], 0.f);
+                o1[r] = (__bf16)fmaxf(d1[r] * inv255 + bch[1][r], 0.f);
+            }
+            *(bf16x4*)(out + q * 32 + 4 * g) = o0;
+            *(bf16x4*)(out + q * 32 + 16 + 4 * g) = o1;
+        }
+        lds_barrier();  // out tile complete
+        if (it < 6) ST();
         u32x4* dst = (u32x4*)(a1 + (size_t)f * 12800);
 #pragma unroll
-        for (int i = 0; i < c1::OUT_PER_T; ++i) {
-            const int c = threadIdx.x + 256 * i;
+        for (int i = 0; i < (c1::OUT_CH + 511) / 512; ++i) {
+            const int c = threadIdx.x + 512 * i;
             if (c < c1::OUT_CH) FI_ST16(((const u32x4*)out)[c], dst + c);
         }
+        issued += stores;
+        m0 = m1;
+        m1 = m2;
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ST();
+    ST_FLUSH();
 }
 
 // ---------------------------------------------------------------------------------
@@ -234,8 +337,9 @@ __global__ __launch_bounds__(256, 1) void conv1_wgrad_fr(const uint8_t* __restri
 
 int conv1_fwd_fr_launch(const uint8_t* frames, const __bf16* w1t, const float* bias, __bf16* a1,
                         int nframes, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(conv1_fwd_fr, dim3(grid), dim3(256), 0, s, frames, w1t, bias, a1, nframes);
+    hipLaunchKernelGGL(conv1_fwd_fr, dim3(grid), dim3(512), 0, s, frames, w1t, bias, a1, nframes);
     FI_HIP_CHECK(hipGetLastError());
+    st_report("conv1_fwd");
     return FI_OK;
 }
 
@@ -488,7 +592,6 @@ constexpr int OUT_CH = 81 * 8;               // 648
 }  // namespace c3
 
 typedef short s16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // wave w DMAs X pieces j = w + 4i (< 11; lanes past pixel 81 read zeros), dY pieces
 // d = w + 4k (< 18) and a3 (mask) pieces m = w + 4k (< 7)
