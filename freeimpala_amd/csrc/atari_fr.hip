@@ -39,8 +39,13 @@ __device__ unsigned long long fi_stamps[256 * 32];
 #include <vector>
 #include <algorithm>
 static void st_report(const char* name) {
-    static int calls = 0;
-    if (++calls != 4) return;
+    static const char* names[8];
+    static int calls[8];
+    int k = 0;
+    while (k < 8 && names[k] && names[k] != name) ++k;
+    if (k == 8) return;
+    names[k] = name;
+    if (++calls[k] != 4) return;
     (void)hipDeviceSynchronize();
     std::vector<unsigned long long> h(256 * 32);
     (void)hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(fi_stamps), h.size() * 8);
@@ -465,6 +470,8 @@ __global__ __launch_bounds__(256, 1) void conv2_bwd_fr(const __bf16* __restrict_
         issued += npw;
         if (i == 0) m0 = issued; else if (i == 1) m1 = issued; else m2 = issued;
     }
+    ST_DECL
+    ST();
     for (int it = 0; it < nmine; ++it) {
         const int f = blockIdx.x + it * gridDim.x;
         const int slot = it % 3;
@@ -472,6 +479,7 @@ __global__ __launch_bounds__(256, 1) void conv2_bwd_fr(const __bf16* __restrict_
         wait_vmcnt(issued - m0);
         lds_barrier();
 
+        if (it < 5) ST();
         // ---------------- weight gradient (taps ky = w, kx = 0..3)
 #pragma unroll
         for (int ms = 0; ms < 6; ++ms) {
@@ -492,6 +500,7 @@ __global__ __launch_bounds__(256, 1) void conv2_bwd_fr(const __bf16* __restrict_
             }
         }
 
+        if (it < 5) ST();
         // ---------------- data gradient, parity class (w>>1, w&1); two row tiles in flight
 #pragma unroll
         for (int rp = 0; rp < 2; ++rp) {
@@ -515,6 +524,7 @@ __global__ __launch_bounds__(256, 1) void conv2_bwd_fr(const __bf16* __restrict_
             }
         }
         lds_barrier();  // dgrad tile complete
+        if (it < 5) ST();
         {  // da1 = (X > 0) * dX in NHWC order: chunk P = pixel P/4, channels 8*(P%4)..+8
             u32x4* dst = (u32x4*)(da1 + (size_t)f * 12800);
 #pragma unroll
@@ -535,6 +545,7 @@ __global__ __launch_bounds__(256, 1) void conv2_bwd_fr(const __bf16* __restrict_
             issued += STORES;  // (wave 0 issues one more; counting fewer only waits longer)
         }
         lds_barrier();  // slot fully consumed
+        if (it < 5) ST();
         int m3 = 0;
         if (it + 3 < nmine) {
             const int fn = blockIdx.x + (it + 3) * gridDim.x;
@@ -547,6 +558,8 @@ __global__ __launch_bounds__(256, 1) void conv2_bwd_fr(const __bf16* __restrict_
         m2 = m3;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ST();
+    ST_FLUSH();
     float* out = slab + (size_t)blockIdx.x * 512 * 64;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -571,6 +584,7 @@ int conv2_bwd_fr_launch(const __bf16* a1, const __bf16* da2, const __bf16* w2d, 
     hipLaunchKernelGGL(conv2_bwd_fr, dim3(grid), dim3(256), 0, s, a1, da2, w2d, da1,
                        slab, cs_slab, nframes);
     FI_HIP_CHECK(hipGetLastError());
+    st_report("conv2_bwd");
     return FI_OK;
 }
 
@@ -593,91 +607,43 @@ constexpr int OUT_CH = 81 * 8;               // 648
 
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 
-// wave w DMAs X pieces j = w + 4i (< 11; lanes past pixel 81 read zeros), dY pieces
-// d = w + 4k (< 18) and a3 (mask) pieces m = w + 4k (< 7)
-__device__ __forceinline__ void c3_issue(const __bf16* x, const __bf16* dy, const __bf16* a3,
-                                         const uint32_t (&dvo)[5], uint32_t slot_lds, int w, int lane) {
-    const fi_i32x4 xr = make_rsrc(x, 10368), dr = make_rsrc(dy, 6272), mr = make_rsrc(a3, 6272);
+// 8 waves, two per SIMD: waves 0-3 compute the weight gradient, waves 4-7 the data gradient
+// of the same frame (their register sets differ, so each role keeps its own: wgrad 160
+// accumulators, dgrad the W3 slice), and one role's LDS waits hide behind the other's MFMAs.
+struct C3Ctx {
+    const __bf16 *a2, *da3, *a3;
+    __bf16* da2;
+    int nframes;
+};
+
+// pieces j = w + 8i (< 36) of frame f: X 0..10, dY 11..28 (zero-bordered), a3 mask 29..35
+__device__ __forceinline__ void c3_issue8(const C3Ctx& c, int f, uint32_t slot_lds, int w, int lane) {
+    const fi_i32x4 xr = make_rsrc(c.a2 + (size_t)f * 5184, 10368);
+    const fi_i32x4 dr = make_rsrc(c.da3 + (size_t)f * 3136, 6272);
+    const fi_i32x4 mr = make_rsrc(c.a3 + (size_t)f * 3136, 6272);
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const int m = w + 4 * k;
-        if (k < 1 || m < c3::NM) blds16(mr, 16 * lane + 1024 * m, slot_lds + c3::XB + c3::DYB + m * 1024);
-    }
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const int j = w + 4 * i;
-        if (i < 2 || j < c3::NX) blds16(xr, 16 * lane + 1024 * j, slot_lds + j * 1024);
-    }
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-        const int d = w + 4 * k;
-        if (k < 4 || d < c3::NDY) blds16(dr, dvo[k], slot_lds + c3::XB + d * 1024);
+    for (int i = 0; i < 5; ++i) {
+        const int j = w + 8 * i;
+        if (j < c3::NX) blds16(xr, 16 * lane + 1024 * j, slot_lds + j * 1024);
+        else if (j < c3::NX + c3::NDY)
+            blds16(dr, dy_piece_off(64 * (j - c3::NX) + lane, 7, 2), slot_lds + c3::XB + (j - c3::NX) * 1024);
+        else if (j < c3::NX + c3::NDY + c3::NM)
+            blds16(mr, 16 * lane + 1024 * (j - c3::NX - c3::NDY), slot_lds + c3::XB + c3::DYB + (j - c3::NX - c3::NDY) * 1024);
     }
 }
 
-__global__ __launch_bounds__(256, 1) void conv3_bwd_fr(const __bf16* __restrict__ a2,
-                                                       const __bf16* __restrict__ da3,  // unmasked
-                                                       const __bf16* __restrict__ a3,   // its mask
-                                                       const __bf16* __restrict__ w3d,  // [64 ci][576]
-                                                       __bf16* __restrict__ da2,
-                                                       float* __restrict__ slab,     // [grid][576][64]
-                                                       float* __restrict__ cs_slab,  // [grid][64]
-                                                       int nframes) {
-    __shared__ __attribute__((aligned(16))) char smem[c3::RING * c3::SLOT + c3::OUTT];
-    const int lane = threadIdx.x & 63;
-    const int w = wave_id();
-    const int g = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3, h = lane >> 5;
+// frame loop shared by both roles: identical barriers, DMA ring, dY mask, masked copy-out
+template <class Work>
+__device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, Work&& work) {
+    const int lane = threadIdx.x & 63, w = wave_id(), tid = threadIdx.x;
     const uint32_t lds0 = lds_addr(smem);
-    __bf16* outt = (__bf16*)(smem + c3::RING * c3::SLOT);
-
-    // dgrad B (16x16x32): lane holds W[k = 32ks + 8g + j][ci = 16w + (lane&15)]
-    s16x8 bw[18];
-#pragma unroll
-    for (int ks = 0; ks < 18; ++ks)
-        bw[ks] = *(const s16x8*)(w3d + (size_t)(16 * w + (lane & 15)) * 576 + 32 * ks + 8 * g);
-
-    // wgrad tap offsets of this wave's k-tiles (wave-uniform): tap = 2i + (w>>1)
-    int toff[5];
-#pragma unroll
-    for (int i = 0; i < 5; ++i) {
-        const int t = min(2 * i + (w >> 1), 8), ky = t / 3, kx = t - 3 * ky;
-        toff[i] = __builtin_amdgcn_readfirstlane(128 * (9 * ky + kx));
-    }
-    const int nkt = (18 - w + 3) / 4;  // 5,5,4,4
-    int ba[4][2], bb[4][2];
-#pragma unroll
-    for (int ms = 0; ms < 4; ++ms)
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-            const int mu = ms * 16 + 8 * (g >> 1) + q + 4 * hh;
-            const int m = min(mu, 48), oy = m / 7, ox = m - 7 * oy;
-            ba[ms][hh] = 128 * (oy * 9 + ox) + 2 * (32 * (w & 1) + 16 * (g & 1) + 4 * p4);
-            const int mb = min(mu, 55), by = mb / 7, bx = mb - 7 * by;  // m >= 49 -> zero border
-            bb[ms][hh] = c3::XB + DP * ((by + 2) * 11 + bx + 2) + 2 * (16 * (g & 1) + 4 * p4);
-        }
-    uint32_t dvo[5];
-#pragma unroll
-    for (int k = 0; k < 5; ++k) dvo[k] = dy_piece_off(64 * (w + 4 * k) + lane, 7, 2);
-    int bd[6];
-#pragma unroll
-    for (int rt = 0; rt < 6; ++rt) {
-        const int pix = min(rt * 16 + (lane & 15), 80), iy = pix / 9, ix = pix - 9 * iy;
-        bd[rt] = c3::XB + DP * ((iy + 2) * 11 + ix + 2 - 24) + 16 * g;
-    }
-
-    f32x16 accw[5][2];
-#pragma unroll
-    for (int i = 0; i < 5; ++i) { accw[i][0] = f32x16{}; accw[i][1] = f32x16{}; }
-    float bsum0 = 0.f, bsum1 = 0.f;
-
-    const int npw = (c3::NX - w + 3) / 4 + (c3::NDY - w + 3) / 4 + (c3::NM - w + 3) / 4;
-    constexpr int STORES = c3::OUT_CH / 256;  // 2
+    const __bf16* outt = (const __bf16*)(smem + c3::RING * c3::SLOT);
+    const int npw = (c3::NX + c3::NDY + c3::NM - w + 7) / 8;  // 5 or 4 pieces per wave
+    const int nst = w <= 2 ? 2 : 1;                           // copy-out stores issued (lower bound)
+    const int nmine = c.nframes > (int)blockIdx.x ? (c.nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
     int issued = 0, m0 = 0, m1 = 0, m2 = 0;
-    const int nmine = nframes > (int)blockIdx.x ? (nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
     for (int i = 0; i < 3 && i < nmine; ++i) {
-        const int f = blockIdx.x + i * gridDim.x;
-        c3_issue(a2 + (size_t)f * 5184, da3 + (size_t)f * 3136, a3 + (size_t)f * 3136, dvo, lds0 + i * c3::SLOT, w,
-                 lane);
+        c3_issue8(c, blockIdx.x + i * gridDim.x, lds0 + i * c3::SLOT, w, lane);
         issued += npw;
         if (i == 0) m0 = issued; else if (i == 1) m1 = issued; else m2 = issued;
     }
@@ -686,75 +652,24 @@ __global__ __launch_bounds__(256, 1) void conv3_bwd_fr(const __bf16* __restrict_
         const int slot = it % 3;
         char* X = smem + slot * c3::SLOT;
         wait_vmcnt(issued - m0);
-        lds_barrier();
-        // ReLU mask of the upstream gradient: dY *= (a3 > 0), 49 px x 8 chunks of 16 B
+        lds_barrier();  // frame landed
+        if (tid < 392) {  // ReLU mask of the upstream gradient: dY *= (a3 > 0)
+            const int p = tid >> 3, ch = tid & 7, py = p / 7, px = p - 7 * py;
+            bf16x8* dyp = (bf16x8*)(X + c3::XB + DP * ((py + 2) * 11 + px + 2) + 16 * ch);
+            const bf16x8 m = *(const bf16x8*)(X + c3::XB + c3::DYB + 128 * p + 16 * ch);
+            bf16x8 v = *dyp;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int qq = threadIdx.x + 256 * i;
-            if (qq < 392) {
-                const int p = qq >> 3, c = qq & 7, py = p / 7, px = p - 7 * py;
-                bf16x8* dyp = (bf16x8*)(X + c3::XB + DP * ((py + 2) * 11 + px + 2) + 16 * c);
-                const bf16x8 m = *(const bf16x8*)(X + c3::XB + c3::DYB + 128 * p + 16 * c);
-                bf16x8 v = *dyp;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) v[j] = (float)m[j] > 0.f ? v[j] : (__bf16)0.f;
-                *dyp = v;
-            }
+            for (int j = 0; j < 8; ++j) v[j] = (float)m[j] > 0.f ? v[j] : (__bf16)0.f;
+            *dyp = v;
         }
-        lds_barrier();
-
-        // ---------------- weight gradient
-#pragma unroll
-        for (int ms = 0; ms < 4; ++ms) {
-            const bf16x8 b0 = tr2(X + bb[ms][0], X + bb[ms][1]);
-            const bf16x8 b1 = tr2(X + bb[ms][0] + 64, X + bb[ms][1] + 64);
-            if (w == 0) {
-                float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) { s0 += (float)b0[j]; s1 += (float)b1[j]; }
-                bsum0 += s0;
-                bsum1 += s1;
-            }
-#pragma unroll
-            for (int i = 0; i < 5; ++i) {
-                if (i < nkt) {
-                    const bf16x8 afr = tr2(X + ba[ms][0] + toff[i], X + ba[ms][1] + toff[i]);
-                    accw[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, b0, accw[i][0], 0, 0, 0);
-                    accw[i][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, b1, accw[i][1], 0, 0, 0);
-                }
-            }
-        }
-
-        // ---------------- data gradient (16x16x32); two row tiles in flight
-#pragma unroll
-        for (int rp = 0; rp < 3; ++rp) {
-            f32x4 acc0 = {}, acc1 = {};
-            const char* base0 = X + bd[2 * rp];
-            const char* base1 = X + bd[2 * rp + 1];
-#pragma unroll
-            for (int ks = 0; ks < 18; ++ks) {
-                const int tap = ks >> 1, ky = tap / 3, kx = tap - 3 * ky;
-                const int off = DP * (24 - (11 * ky + kx)) + 64 * (ks & 1);
-                const s16x8 a0 = *(const s16x8*)(base0 + off);
-                const s16x8 a1 = *(const s16x8*)(base1 + off);
-                acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a0),
-                                                              __builtin_bit_cast(bf16x8, bw[ks]), acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a1),
-                                                              __builtin_bit_cast(bf16x8, bw[ks]), acc1, 0, 0, 0);
-            }
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = rp * 32 + 4 * g + r;
-                outt[row * 64 + 16 * w + (lane & 15)] = (__bf16)acc0[r];
-                if (row + 16 < 81) outt[(row + 16) * 64 + 16 * w + (lane & 15)] = (__bf16)acc1[r];
-            }
-        }
+        lds_barrier();  // masked dY visible
+        work(X);
         lds_barrier();  // dgrad tile complete
         {
-            u32x4* dst = (u32x4*)(da2 + (size_t)f * 5184);
+            u32x4* dst = (u32x4*)(c.da2 + (size_t)f * 5184);
 #pragma unroll
-            for (int i = 0; i < (c3::OUT_CH + 255) / 256; ++i) {
-                const int P = threadIdx.x + 256 * i;
+            for (int i = 0; i < 2; ++i) {
+                const int P = tid + 512 * i;
                 if (P < c3::OUT_CH) {
                     const bf16x8 v = *(const bf16x8*)(outt + 8 * P);
                     const bf16x8 m = *(const bf16x8*)(X + 16 * P);
@@ -764,14 +679,12 @@ __global__ __launch_bounds__(256, 1) void conv3_bwd_fr(const __bf16* __restrict_
                     FI_ST16(__builtin_bit_cast(u32x4, o), dst + P);
                 }
             }
-            issued += STORES;
+            issued += nst;
         }
         lds_barrier();  // slot fully consumed
         int m3 = 0;
         if (it + 3 < nmine) {
-            const int fn = blockIdx.x + (it + 3) * gridDim.x;
-            c3_issue(a2 + (size_t)fn * 5184, da3 + (size_t)fn * 3136, a3 + (size_t)fn * 3136, dvo,
-                     lds0 + slot * c3::SLOT, w, lane);
+            c3_issue8(c, blockIdx.x + (it + 3) * gridDim.x, lds0 + slot * c3::SLOT, w, lane);
             issued += npw;
             m3 = issued;
         }
@@ -780,34 +693,136 @@ __global__ __launch_bounds__(256, 1) void conv3_bwd_fr(const __bf16* __restrict_
         m2 = m3;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    float* out = slab + (size_t)blockIdx.x * 576 * 64;
+}
+
+__global__ __launch_bounds__(512, 2) void conv3_bwd_fr(const __bf16* __restrict__ a2,
+                                                       const __bf16* __restrict__ da3,  // unmasked
+                                                       const __bf16* __restrict__ a3,   // its mask
+                                                       const __bf16* __restrict__ w3d,  // [64 ci][576]
+                                                       __bf16* __restrict__ da2,
+                                                       float* __restrict__ slab,     // [grid][576][64]
+                                                       float* __restrict__ cs_slab,  // [grid][64]
+                                                       int nframes) {
+    __shared__ __attribute__((aligned(16))) char smem[c3::RING * c3::SLOT + c3::OUTT];
+    const int lane = threadIdx.x & 63;
+    const int w = wave_id(), wr = w & 3;
+    const int g = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3, h = lane >> 5;
+    const C3Ctx ctx{a2, da3, a3, da2, nframes};
+
+    if (w < 4) {
+        // ---------------- weight gradient: k-tiles kt = wr + 4i = (tap 2i + (wr>>1), channel half wr&1)
+        int toff[5];
 #pragma unroll
-    for (int i = 0; i < 5; ++i) {
-        if (i < nkt) {
-            const int kt = w + 4 * i;
+        for (int i = 0; i < 5; ++i) {
+            const int t = min(2 * i + (wr >> 1), 8), ky = t / 3, kx = t - 3 * ky;
+            toff[i] = __builtin_amdgcn_readfirstlane(128 * (9 * ky + kx));
+        }
+        const int nkt = (18 - wr + 3) / 4;  // 5,5,4,4
+        int ba[4][2], bb[4][2];
 #pragma unroll
-            for (int ct = 0; ct < 2; ++ct)
+        for (int ms = 0; ms < 4; ++ms)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int k = 32 * kt + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    out[k * 64 + 32 * ct + (lane & 31)] = accw[i][ct][r];
+            for (int hh = 0; hh < 2; ++hh) {
+                const int mu = ms * 16 + 8 * (g >> 1) + q + 4 * hh;
+                const int m = min(mu, 48), oy = m / 7, ox = m - 7 * oy;
+                ba[ms][hh] = 128 * (oy * 9 + ox) + 2 * (32 * (wr & 1) + 16 * (g & 1) + 4 * p4);
+                const int mb = min(mu, 55), by = mb / 7, bx = mb - 7 * by;  // m >= 49 -> zero border
+                bb[ms][hh] = c3::XB + DP * ((by + 2) * 11 + bx + 2) + 2 * (16 * (g & 1) + 4 * p4);
+            }
+        f32x16 accw[5][2];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) { accw[i][0] = f32x16{}; accw[i][1] = f32x16{}; }
+        float bsum0 = 0.f, bsum1 = 0.f;
+        c3_frames(ctx, smem, [&](const char* X) {
+#pragma unroll
+            for (int ms = 0; ms < 4; ++ms) {
+                const bf16x8 b0 = tr2(X + bb[ms][0], X + bb[ms][1]);
+                const bf16x8 b1 = tr2(X + bb[ms][0] + 64, X + bb[ms][1] + 64);
+                if (wr == 0) {
+                    float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) { s0 += (float)b0[j]; s1 += (float)b1[j]; }
+                    bsum0 += s0;
+                    bsum1 += s1;
                 }
+#pragma unroll
+                for (int i = 0; i < 5; ++i) {
+                    if (i < nkt) {
+                        const bf16x8 afr = tr2(X + ba[ms][0] + toff[i], X + ba[ms][1] + toff[i]);
+                        accw[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, b0, accw[i][0], 0, 0, 0);
+                        accw[i][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, b1, accw[i][1], 0, 0, 0);
+                    }
+                }
+            }
+        });
+        float* out = slab + (size_t)blockIdx.x * 576 * 64;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            if (i < nkt) {
+                const int kt = wr + 4 * i;
+#pragma unroll
+                for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int k = 32 * kt + (r & 3) + 8 * (r >> 2) + 4 * h;
+                        out[k * 64 + 32 * ct + (lane & 31)] = accw[i][ct][r];
+                    }
+            }
         }
-    }
-    if (w == 0) {
-        const float o0 = __shfl_xor(bsum0, 32, 64), o1 = __shfl_xor(bsum1, 32, 64);
-        if (lane < 32) {
-            cs_slab[(size_t)blockIdx.x * 64 + lane] = bsum0 + o0;
-            cs_slab[(size_t)blockIdx.x * 64 + 32 + lane] = bsum1 + o1;
+        if (wr == 0) {
+            const float o0 = __shfl_xor(bsum0, 32, 64), o1 = __shfl_xor(bsum1, 32, 64);
+            if (lane < 32) {
+                cs_slab[(size_t)blockIdx.x * 64 + lane] = bsum0 + o0;
+                cs_slab[(size_t)blockIdx.x * 64 + 32 + lane] = bsum1 + o1;
+            }
         }
+    } else {
+        // ---------------- data gradient (16x16x32): input channels 16wr..+16, all 6 row tiles
+        __bf16* outt = (__bf16*)(smem + c3::RING * c3::SLOT);
+        s16x8 bw[18];  // lane holds W[k = 32ks + 8g + j][ci = 16wr + (lane&15)]
+#pragma unroll
+        for (int ks = 0; ks < 18; ++ks)
+            bw[ks] = *(const s16x8*)(w3d + (size_t)(16 * wr + (lane & 15)) * 576 + 32 * ks + 8 * g);
+        int bd[6];
+#pragma unroll
+        for (int rt = 0; rt < 6; ++rt) {
+            const int pix = min(rt * 16 + (lane & 15), 80), iy = pix / 9, ix = pix - 9 * iy;
+            bd[rt] = c3::XB + DP * ((iy + 2) * 11 + ix + 2 - 24) + 16 * g;
+        }
+        c3_frames(ctx, smem, [&](const char* X) {
+#pragma unroll
+            for (int rp = 0; rp < 3; ++rp) {
+                f32x4 acc0 = {}, acc1 = {};
+                const char* base0 = X + bd[2 * rp];
+                const char* base1 = X + bd[2 * rp + 1];
+#pragma unroll
+                for (int ks = 0; ks < 18; ++ks) {
+                    const int tap = ks >> 1, ky = tap / 3, kx = tap - 3 * ky;
+                    const int off = DP * (24 - (11 * ky + kx)) + 64 * (ks & 1);
+                    const s16x8 a0 = *(const s16x8*)(base0 + off);
+                    const s16x8 a1 = *(const s16x8*)(base1 + off);
+                    acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a0),
+                                                                  __builtin_bit_cast(bf16x8, bw[ks]), acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a1),
+                                                                  __builtin_bit_cast(bf16x8, bw[ks]), acc1, 0, 0, 0);
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = rp * 32 + 4 * g + r;
+                    outt[row * 64 + 16 * wr + (lane & 15)] = (__bf16)acc0[r];
+                    if (row + 16 < 81) outt[(row + 16) * 64 + 16 * wr + (lane & 15)] = (__bf16)acc1[r];
+                }
+            }
+        });
     }
 }
 
 int conv3_bwd_fr_launch(const __bf16* a2, const __bf16* da3, const __bf16* a3, const __bf16* w3d, __bf16* da2,
                         float* slab, float* cs_slab, int nframes, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(conv3_bwd_fr, dim3(grid), dim3(256), 0, s, a2, da3, a3, w3d, da2,
+    hipLaunchKernelGGL(conv3_bwd_fr, dim3(grid), dim3(512), 0, s, a2, da3, a3, w3d, da2,
                        slab, cs_slab, nframes);
     FI_HIP_CHECK(hipGetLastError());
+    st_report("conv3_bwd");
     return FI_OK;
 }
 
