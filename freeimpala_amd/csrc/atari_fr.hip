@@ -398,143 +398,64 @@ constexpr int OUTT = 4 * 100 * 64;           // dgrad tile [class][100][32 ci] b
 constexpr int OUT_CH = XB / 16;              // 1600
 }  // namespace c2
 
-// wave w DMAs X pieces j = w + 4i (< 25) and dY pieces d = w + 4k (< 18)
-__device__ __forceinline__ void c2_issue(const __bf16* x, const __bf16* dy, const uint32_t (&dvo)[5],
-                                         uint32_t slot_lds, int w, int lane) {
-    const fi_i32x4 xr = make_rsrc(x, 25600), dr = make_rsrc(dy, 10368);
+// 8 waves, two per SIMD: waves 0-3 compute the weight gradient (wave = kernel row ky),
+// waves 4-7 the data gradient (wave = parity class), sharing one frame pipeline.
+struct C2Ctx {
+    const __bf16 *a1, *da2;
+    __bf16* da1;
+    int nframes;
+};
+
+// pieces j = w + 8i (< 43) of frame f: X 0..24, dY 25..42 (zero-bordered)
+__device__ __forceinline__ void c2_issue8(const C2Ctx& c, const uint32_t* dyo, int f, uint32_t slot_lds, int w,
+                                          int lane) {
+    const fi_i32x4 xr = make_rsrc(c.a1 + (size_t)f * 12800, 25600);
+    const fi_i32x4 dr = make_rsrc(c.da2 + (size_t)f * 5184, 10368);
 #pragma unroll
-    for (int i = 0; i < 7; ++i) {
-        const int j = w + 4 * i;
-        if (i < 6 || j < c2::NX) blds16(xr, 16 * lane + 1024 * j, slot_lds + j * 1024);
-    }
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-        const int d = w + 4 * k;
-        if (k < 4 || d < c2::NDY) blds16(dr, dvo[k], slot_lds + c2::XB + d * 1024);
+    for (int i = 0; i < 6; ++i) {
+        const int j = w + 8 * i;
+        if (j < c2::NX) blds16(xr, 16 * lane + 1024 * j, slot_lds + j * 1024);
+        else if (j < c2::NX + c2::NDY)
+            blds16(dr, dyo[64 * (j - c2::NX) + lane], slot_lds + c2::XB + (j - c2::NX) * 1024);
     }
 }
 
-__global__ __launch_bounds__(256, 1) void conv2_bwd_fr(const __bf16* __restrict__ a1,
-                                                       const __bf16* __restrict__ da2,
-                                                       const __bf16* __restrict__ w2d,  // [4][32][256]
-                                                       __bf16* __restrict__ da1,
-                                                       float* __restrict__ slab,     // [grid][512][64]
-                                                       float* __restrict__ cs_slab,  // [grid][64]
-                                                       int nframes) {
-    __shared__ __attribute__((aligned(16))) char smem[c2::RING * c2::SLOT + c2::OUTT];
-    const int lane = threadIdx.x & 63;
-    const int w = wave_id();
-    const int g = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3, h = lane >> 5, col = lane & 31;
+template <class Work>
+__device__ __forceinline__ void c2_frames(const C2Ctx& c, char* smem, Work&& work) {
+    const int lane = threadIdx.x & 63, w = wave_id(), tid = threadIdx.x;
     const uint32_t lds0 = lds_addr(smem);
-    __bf16* outt = (__bf16*)(smem + c2::RING * c2::SLOT);
-
-    // dgrad B fragments (class w): W[k = 16ks + 8h + j][ci = col]
-    bf16x8 bw[16];
-#pragma unroll
-    for (int ks = 0; ks < 16; ++ks) bw[ks] = *(const bf16x8*)(w2d + ((size_t)(w * 32 + col)) * 256 + ks * 16 + h * 8);
-
-    // ---- per-lane base offsets (relative to a ring slot); everything else is immediate
-    int ba[6][2], bb[6][2];  // wgrad A (X, tap ky = w, kx = 0 -> +64*kx) / wgrad B (dY, ct -> +64)
-#pragma unroll
-    for (int ms = 0; ms < 6; ++ms)
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-            const int mu = ms * 16 + 8 * (g >> 1) + q + 4 * hh;
-            const int m = min(mu, 80), oy = m / 9, ox = m - 9 * oy;
-            ba[ms][hh] = 64 * ((2 * oy + w) * 20 + 2 * ox) + 2 * (16 * (g & 1) + 4 * p4);
-            const int mb = min(mu, 89), by = mb / 9, bx = mb - 9 * by;  // m >= 81 -> zero border
-            bb[ms][hh] = c2::XB + DP * ((by + 1) * 11 + bx + 1) + 2 * (16 * (g & 1) + 4 * p4);
-        }
-    uint32_t dvo[5];
-#pragma unroll
-    for (int k = 0; k < 5; ++k) dvo[k] = dy_piece_off(64 * (w + 4 * k) + lane, 9, 1);
-    int bd[4];  // dgrad A: dY row of (iyq - ty, ixq - tx) = base - 144*(11 ty + tx)
-#pragma unroll
-    for (int rt = 0; rt < 4; ++rt) {
-        const int r = min(rt * 32 + col, 99), iyq = r / 10, ixq = r - 10 * iyq;
-        bd[rt] = c2::XB + DP * ((iyq + 1) * 11 + ixq + 1 - 12) + 16 * h;
-    }
-
-    f32x16 accw[4][2];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) { accw[t][0] = f32x16{}; accw[t][1] = f32x16{}; }
-    float bsum0 = 0.f, bsum1 = 0.f;
-
-    const int npw = (c2::NX - w + 3) / 4 + (c2::NDY - w + 3) / 4;
-    constexpr int STORES = c2::OUT_CH / 256;   // 6 store instructions every wave issues
+    const __bf16* outt = (const __bf16*)(smem + c2::RING * c2::SLOT);
+    // byte offsets of every zero-bordered dY piece (FI_OOB for border / pad slots)
+    uint32_t* dyo = (uint32_t*)(smem + c2::RING * c2::SLOT + c2::OUTT);
+    for (int i = tid; i < c2::NDY * 64; i += 512) dyo[i] = dy_piece_off(i, 9, 1);
+    __syncthreads();
+    const int npw = (c2::NX + c2::NDY - w + 7) / 8;  // 6 or 5 pieces per wave
+    const int nst = w == 0 ? 4 : 3;                  // copy-out stores issued (lower bound)
+    const int nmine = c.nframes > (int)blockIdx.x ? (c.nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
     int issued = 0, m0 = 0, m1 = 0, m2 = 0;
-    const int nmine = nframes > (int)blockIdx.x ? (nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
     for (int i = 0; i < 3 && i < nmine; ++i) {
-        const int f = blockIdx.x + i * gridDim.x;
-        c2_issue(a1 + (size_t)f * 12800, da2 + (size_t)f * 5184, dvo, lds0 + i * c2::SLOT, w, lane);
+        c2_issue8(c, dyo, blockIdx.x + i * gridDim.x, lds0 + i * c2::SLOT, w, lane);
         issued += npw;
         if (i == 0) m0 = issued; else if (i == 1) m1 = issued; else m2 = issued;
     }
-    ST_DECL
-    ST();
     for (int it = 0; it < nmine; ++it) {
         const int f = blockIdx.x + it * gridDim.x;
         const int slot = it % 3;
         char* X = smem + slot * c2::SLOT;
         wait_vmcnt(issued - m0);
-        lds_barrier();
-
-        if (it < 5) ST();
-        // ---------------- weight gradient (taps ky = w, kx = 0..3)
-#pragma unroll
-        for (int ms = 0; ms < 6; ++ms) {
-            const bf16x8 b0 = tr2(X + bb[ms][0], X + bb[ms][1]);
-            const bf16x8 b1 = tr2(X + bb[ms][0] + 64, X + bb[ms][1] + 64);
-            if (w == 0) {
-                float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) { s0 += (float)b0[j]; s1 += (float)b1[j]; }
-                bsum0 += s0;
-                bsum1 += s1;
-            }
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const bf16x8 afr = tr2(X + ba[ms][0] + 64 * t, X + ba[ms][1] + 64 * t);
-                accw[t][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, b0, accw[t][0], 0, 0, 0);
-                accw[t][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, b1, accw[t][1], 0, 0, 0);
-            }
-        }
-
-        if (it < 5) ST();
-        // ---------------- data gradient, parity class (w>>1, w&1); two row tiles in flight
-#pragma unroll
-        for (int rp = 0; rp < 2; ++rp) {
-            f32x16 acc0 = {}, acc1 = {};
-            const char* base0 = X + bd[2 * rp];
-            const char* base1 = X + bd[2 * rp + 1];
-#pragma unroll
-            for (int ks = 0; ks < 16; ++ks) {
-                const int tap = ks >> 2, ty = tap >> 1, tx = tap & 1;
-                const int off = DP * (12 - (11 * ty + tx)) + 32 * (ks & 3);
-                const bf16x8 a0 = *(const bf16x8*)(base0 + off);
-                const bf16x8 a1 = *(const bf16x8*)(base1 + off);
-                acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bw[ks], acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bw[ks], acc1, 0, 0, 0);
-            }
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int ri = rp * 64 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                outt[(w * 100 + ri) * 32 + col] = (__bf16)acc0[r];
-                if (ri + 32 < 100) outt[(w * 100 + ri + 32) * 32 + col] = (__bf16)acc1[r];
-            }
-        }
+        lds_barrier();  // frame landed
+        work(X);
         lds_barrier();  // dgrad tile complete
-        if (it < 5) ST();
         {  // da1 = (X > 0) * dX in NHWC order: chunk P = pixel P/4, channels 8*(P%4)..+8
-            u32x4* dst = (u32x4*)(da1 + (size_t)f * 12800);
+            u32x4* dst = (u32x4*)(c.da1 + (size_t)f * 12800);
 #pragma unroll
-            for (int i = 0; i < (c2::OUT_CH + 255) / 256; ++i) {
-                const int P = threadIdx.x + 256 * i;
+            for (int i = 0; i < (c2::OUT_CH + 511) / 512; ++i) {
+                const int P = tid + 512 * i;
                 if (P < c2::OUT_CH) {
-                    const int pix = P >> 2, c = P & 3;
+                    const int pix = P >> 2, ch = P & 3;
                     const int iy = pix / 20, ix = pix - iy * 20;
                     const int cls = ((iy & 1) << 1) | (ix & 1), ri = (iy >> 1) * 10 + (ix >> 1);
-                    const bf16x8 v = *(const bf16x8*)(outt + (cls * 100 + ri) * 32 + 8 * c);
+                    const bf16x8 v = *(const bf16x8*)(outt + (cls * 100 + ri) * 32 + 8 * ch);
                     const bf16x8 m = *(const bf16x8*)(X + 16 * P);
                     bf16x8 o;
 #pragma unroll
@@ -542,14 +463,15 @@ __global__ __launch_bounds__(256, 1) void conv2_bwd_fr(const __bf16* __restrict_
                     FI_ST16(__builtin_bit_cast(u32x4, o), dst + P);
                 }
             }
-            issued += STORES;  // (wave 0 issues one more; counting fewer only waits longer)
+            issued += nst;
         }
         lds_barrier();  // slot fully consumed
-        if (it < 5) ST();
         int m3 = 0;
         if (it + 3 < nmine) {
-            const int fn = blockIdx.x + (it + 3) * gridDim.x;
-            c2_issue(a1 + (size_t)fn * 12800, da2 + (size_t)fn * 5184, dvo, lds0 + slot * c2::SLOT, w, lane);
+            // the previous frame's copy-out stores drain before the next DMA pieces queue
+            // behind them (measured: slightly faster than letting them overlap)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            c2_issue8(c, dyo, blockIdx.x + (it + 3) * gridDim.x, lds0 + slot * c2::SLOT, w, lane);
             issued += npw;
             m3 = issued;
         }
@@ -558,30 +480,117 @@ __global__ __launch_bounds__(256, 1) void conv2_bwd_fr(const __bf16* __restrict_
         m2 = m3;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    ST();
-    ST_FLUSH();
-    float* out = slab + (size_t)blockIdx.x * 512 * 64;
+}
+
+__global__ __launch_bounds__(512, 2) void conv2_bwd_fr(const __bf16* __restrict__ a1,
+                                                       const __bf16* __restrict__ da2,
+                                                       const __bf16* __restrict__ w2d,  // [4][32][256]
+                                                       __bf16* __restrict__ da1,
+                                                       float* __restrict__ slab,     // [grid][512][64]
+                                                       float* __restrict__ cs_slab,  // [grid][64]
+                                                       int nframes) {
+    __shared__ __attribute__((aligned(16))) char smem[c2::RING * c2::SLOT + c2::OUTT + c2::NDY * 64 * 4];
+    const int lane = threadIdx.x & 63;
+    const int w = wave_id(), wr = w & 3;
+    const int g = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3, h = lane >> 5, col = lane & 31;
+    const C2Ctx ctx{a1, da2, da1, nframes};
+
+    if (w < 4) {
+        // ---------------- weight gradient: taps ky = wr, kx = 0..3 (A base + 64 kx), co halves ct
+        int ba[6][2], bb[6][2];
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+        for (int ms = 0; ms < 6; ++ms)
 #pragma unroll
-        for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int k = 128 * w + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
-                out[k * 64 + 32 * ct + col] = accw[t][ct][r];
+            for (int hh = 0; hh < 2; ++hh) {
+                const int mu = ms * 16 + 8 * (g >> 1) + q + 4 * hh;
+                const int m = min(mu, 80), oy = m / 9, ox = m - 9 * oy;
+                ba[ms][hh] = 64 * ((2 * oy + wr) * 20 + 2 * ox) + 2 * (16 * (g & 1) + 4 * p4);
+                const int mb = min(mu, 89), by = mb / 9, bx = mb - 9 * by;  // m >= 81 -> zero border
+                bb[ms][hh] = c2::XB + DP * ((by + 1) * 11 + bx + 1) + 2 * (16 * (g & 1) + 4 * p4);
             }
-    if (w == 0) {  // lanes l and l+32 hold the same co (16*(g&1) + (l&15)), other m half
-        const float o0 = __shfl_xor(bsum0, 32, 64), o1 = __shfl_xor(bsum1, 32, 64);
-        if (lane < 32) {
-            cs_slab[(size_t)blockIdx.x * 64 + lane] = bsum0 + o0;
-            cs_slab[(size_t)blockIdx.x * 64 + 32 + lane] = bsum1 + o1;
+        f32x16 accw[4][2];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) { accw[t][0] = f32x16{}; accw[t][1] = f32x16{}; }
+        float bsum0 = 0.f, bsum1 = 0.f;
+        c2_frames(ctx, smem, [&](const char* X) {
+#pragma unroll
+            for (int ms = 0; ms < 6; ++ms) {
+                const bf16x8 b0 = tr2(X + bb[ms][0], X + bb[ms][1]);
+                const bf16x8 b1 = tr2(X + bb[ms][0] + 64, X + bb[ms][1] + 64);
+                if (wr == 0) {
+                    float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) { s0 += (float)b0[j]; s1 += (float)b1[j]; }
+                    bsum0 += s0;
+                    bsum1 += s1;
+                }
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const bf16x8 afr = tr2(X + ba[ms][0] + 64 * t, X + ba[ms][1] + 64 * t);
+                    accw[t][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, b0, accw[t][0], 0, 0, 0);
+                    accw[t][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, b1, accw[t][1], 0, 0, 0);
+                }
+            }
+        });
+        float* out = slab + (size_t)blockIdx.x * 512 * 64;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int k = 128 * wr + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    out[k * 64 + 32 * ct + col] = accw[t][ct][r];
+                }
+        if (wr == 0) {  // lanes l and l+32 hold the same co (16*(g&1) + (l&15)), other m half
+            const float o0 = __shfl_xor(bsum0, 32, 64), o1 = __shfl_xor(bsum1, 32, 64);
+            if (lane < 32) {
+                cs_slab[(size_t)blockIdx.x * 64 + lane] = bsum0 + o0;
+                cs_slab[(size_t)blockIdx.x * 64 + 32 + lane] = bsum1 + o1;
+            }
         }
+    } else {
+        // ---------------- data gradient, parity class (wr>>1, wr&1); two row tiles in flight
+        __bf16* outt = (__bf16*)(smem + c2::RING * c2::SLOT);
+        bf16x8 bw[16];  // W[k = 16ks + 8h + j][ci = col] of class wr
+#pragma unroll
+        for (int ks = 0; ks < 16; ++ks)
+            bw[ks] = *(const bf16x8*)(w2d + ((size_t)(wr * 32 + col)) * 256 + ks * 16 + h * 8);
+        int bd[4];  // dY row of (iyq - ty, ixq - tx) = base - 144*(11 ty + tx)
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt) {
+            const int r = min(rt * 32 + col, 99), iyq = r / 10, ixq = r - 10 * iyq;
+            bd[rt] = c2::XB + DP * ((iyq + 1) * 11 + ixq + 1 - 12) + 16 * h;
+        }
+        c2_frames(ctx, smem, [&](const char* X) {
+#pragma unroll
+            for (int rp = 0; rp < 2; ++rp) {
+                f32x16 acc0 = {}, acc1 = {};
+                const char* base0 = X + bd[2 * rp];
+                const char* base1 = X + bd[2 * rp + 1];
+#pragma unroll
+                for (int ks = 0; ks < 16; ++ks) {
+                    const int tap = ks >> 2, ty = tap >> 1, tx = tap & 1;
+                    const int off = DP * (12 - (11 * ty + tx)) + 32 * (ks & 3);
+                    const bf16x8 a0 = *(const bf16x8*)(base0 + off);
+                    const bf16x8 a1v = *(const bf16x8*)(base1 + off);
+                    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bw[ks], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1v, bw[ks], acc1, 0, 0, 0);
+                }
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int ri = rp * 64 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    outt[(wr * 100 + ri) * 32 + col] = (__bf16)acc0[r];
+                    if (ri + 32 < 100) outt[(wr * 100 + ri + 32) * 32 + col] = (__bf16)acc1[r];
+                }
+            }
+        });
     }
 }
 
 int conv2_bwd_fr_launch(const __bf16* a1, const __bf16* da2, const __bf16* w2d, __bf16* da1, float* slab,
                         float* cs_slab, int nframes, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(conv2_bwd_fr, dim3(grid), dim3(256), 0, s, a1, da2, w2d, da1,
+    hipLaunchKernelGGL(conv2_bwd_fr, dim3(grid), dim3(512), 0, s, a1, da2, w2d, da1,
                        slab, cs_slab, nframes);
     FI_HIP_CHECK(hipGetLastError());
     st_report("conv2_bwd");
@@ -617,7 +626,8 @@ struct C3Ctx {
 };
 
 // pieces j = w + 8i (< 36) of frame f: X 0..10, dY 11..28 (zero-bordered), a3 mask 29..35
-__device__ __forceinline__ void c3_issue8(const C3Ctx& c, int f, uint32_t slot_lds, int w, int lane) {
+__device__ __forceinline__ void c3_issue8(const C3Ctx& c, const uint32_t* dyo, int f, uint32_t slot_lds, int w,
+                                          int lane) {
     const fi_i32x4 xr = make_rsrc(c.a2 + (size_t)f * 5184, 10368);
     const fi_i32x4 dr = make_rsrc(c.da3 + (size_t)f * 3136, 6272);
     const fi_i32x4 mr = make_rsrc(c.a3 + (size_t)f * 3136, 6272);
@@ -626,7 +636,7 @@ __device__ __forceinline__ void c3_issue8(const C3Ctx& c, int f, uint32_t slot_l
         const int j = w + 8 * i;
         if (j < c3::NX) blds16(xr, 16 * lane + 1024 * j, slot_lds + j * 1024);
         else if (j < c3::NX + c3::NDY)
-            blds16(dr, dy_piece_off(64 * (j - c3::NX) + lane, 7, 2), slot_lds + c3::XB + (j - c3::NX) * 1024);
+            blds16(dr, dyo[64 * (j - c3::NX) + lane], slot_lds + c3::XB + (j - c3::NX) * 1024);
         else if (j < c3::NX + c3::NDY + c3::NM)
             blds16(mr, 16 * lane + 1024 * (j - c3::NX - c3::NDY), slot_lds + c3::XB + c3::DYB + (j - c3::NX - c3::NDY) * 1024);
     }
@@ -638,12 +648,16 @@ __device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, Work&& wor
     const int lane = threadIdx.x & 63, w = wave_id(), tid = threadIdx.x;
     const uint32_t lds0 = lds_addr(smem);
     const __bf16* outt = (const __bf16*)(smem + c3::RING * c3::SLOT);
+    // byte offsets of every zero-bordered dY piece (FI_OOB for border / pad slots)
+    uint32_t* dyo = (uint32_t*)(smem + c3::RING * c3::SLOT + c3::OUTT);
+    for (int i = tid; i < c3::NDY * 64; i += 512) dyo[i] = dy_piece_off(i, 7, 2);
+    __syncthreads();
     const int npw = (c3::NX + c3::NDY + c3::NM - w + 7) / 8;  // 5 or 4 pieces per wave
     const int nst = w <= 2 ? 2 : 1;                           // copy-out stores issued (lower bound)
     const int nmine = c.nframes > (int)blockIdx.x ? (c.nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
     int issued = 0, m0 = 0, m1 = 0, m2 = 0;
     for (int i = 0; i < 3 && i < nmine; ++i) {
-        c3_issue8(c, blockIdx.x + i * gridDim.x, lds0 + i * c3::SLOT, w, lane);
+        c3_issue8(c, dyo, blockIdx.x + i * gridDim.x, lds0 + i * c3::SLOT, w, lane);
         issued += npw;
         if (i == 0) m0 = issued; else if (i == 1) m1 = issued; else m2 = issued;
     }
@@ -684,7 +698,10 @@ __device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, Work&& wor
         lds_barrier();  // slot fully consumed
         int m3 = 0;
         if (it + 3 < nmine) {
-            c3_issue8(c, blockIdx.x + (it + 3) * gridDim.x, lds0 + slot * c3::SLOT, w, lane);
+            // the previous frame's copy-out stores drain before the next DMA pieces queue
+            // behind them (measured: slightly faster than letting them overlap)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            c3_issue8(c, dyo, blockIdx.x + (it + 3) * gridDim.x, lds0 + slot * c3::SLOT, w, lane);
             issued += npw;
             m3 = issued;
         }
@@ -703,7 +720,7 @@ __global__ __launch_bounds__(512, 2) void conv3_bwd_fr(const __bf16* __restrict_
                                                        float* __restrict__ slab,     // [grid][576][64]
                                                        float* __restrict__ cs_slab,  // [grid][64]
                                                        int nframes) {
-    __shared__ __attribute__((aligned(16))) char smem[c3::RING * c3::SLOT + c3::OUTT];
+    __shared__ __attribute__((aligned(16))) char smem[c3::RING * c3::SLOT + c3::OUTT + c3::NDY * 64 * 4];
     const int lane = threadIdx.x & 63;
     const int w = wave_id(), wr = w & 3;
     const int g = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3, h = lane >> 5;

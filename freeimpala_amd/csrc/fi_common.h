@@ -84,6 +84,13 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_base) {
 #define FI_ST16(v, p) __builtin_nontemporal_store((v), (p))
 #endif
 
+// Opaque copy: the compiler must assume x changed here, so values derived from it are
+// recomputed after this point instead of being hoisted (and spilled) out of a loop.
+__device__ __forceinline__ int fi_opaque(int x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
 // Raw buffer descriptor (stride 0, range-checked to `bytes`) from wave-uniform inputs.
 typedef int fi_i32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ fi_i32x4 make_rsrc(const void* base, uint32_t bytes) {
