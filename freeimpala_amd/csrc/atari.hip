@@ -585,6 +585,10 @@ struct AtariImpl {
 
 int conv1_fwd_fr_launch(const uint8_t* frames, const __bf16* w1t, const float* bias, __bf16* a1,
                         int nframes, int grid, hipStream_t s);
+int conv2_fwd_fr_launch(const __bf16* a1, const __bf16* w2t, const float* bias, __bf16* a2, int nframes,
+                        int grid, hipStream_t s);
+int conv3_fwd_fr_launch(const __bf16* a2, const __bf16* w3t, const float* bias, __bf16* a3, int nframes,
+                        int grid, hipStream_t s);
 int conv1_wgrad_fr_launch(const uint8_t* frames, const __bf16* da1, float* slab, float* cs_slab,
                           int nframes, int grid, hipStream_t s);
 int conv2_bwd_fr_launch(const __bf16* a1, const __bf16* da2, const __bf16* w2d, __bf16* da1, float* slab,
@@ -691,10 +695,16 @@ int atari_forward(AtariNet* n, const uint8_t* frames, float* logits, float* valu
     } else { TagScope ts(tg, "conv1_fwd"); rc = gemm<256, 32, 4, 1>(Conv1Gather{frames, N * P1}, RowsBf16{I->wb.c1T, C1O, C1K},
                              EpiAct{I->a1, C1O, p + o.c1b, 1.0f / 255.0f}, N * P1, C1O, C1K, s); }
     if (rc) return rc;
-    { TagScope ts(tg, "conv2_fwd"); rc = gemm<128, 64, 2, 2>(ConvGather<20, 32, 4, 2, 9>{I->a1, N * P2}, RowsBf16{I->wb.c2T, C2O, C2K},
+    if (I->fr) {
+        TagScope ts(tg, "conv2_fwd");
+        rc = conv2_fwd_fr_launch(I->a1, I->wb.c2T, p + o.c2b, I->a2, N, std::min(N, FR_GRID), s);
+    } else { TagScope ts(tg, "conv2_fwd"); rc = gemm<128, 64, 2, 2>(ConvGather<20, 32, 4, 2, 9>{I->a1, N * P2}, RowsBf16{I->wb.c2T, C2O, C2K},
                              EpiAct{I->a2, C2O, p + o.c2b, 1.0f}, N * P2, C2O, C2K, s); }
     if (rc) return rc;
-    { TagScope ts(tg, "conv3_fwd"); rc = gemm<128, 64, 2, 2>(ConvGather<9, 64, 3, 1, 7>{I->a2, N * P3}, RowsBf16{I->wb.c3T, C3O, C3K},
+    if (I->fr) {
+        TagScope ts(tg, "conv3_fwd");
+        rc = conv3_fwd_fr_launch(I->a2, I->wb.c3T, p + o.c3b, I->a3, N, std::min(N, FR_GRID), s);
+    } else { TagScope ts(tg, "conv3_fwd"); rc = gemm<128, 64, 2, 2>(ConvGather<9, 64, 3, 1, 7>{I->a2, N * P3}, RowsBf16{I->wb.c3T, C3O, C3K},
                              EpiAct{I->a3, C3O, p + o.c3b, 1.0f}, N * P3, C3O, C3K, s); }
     if (rc) return rc;
     { TagScope ts(tg, "fc_fwd"); rc = fc_blaslt_forward(I->fc, I->a3, I->wb.fcB, p + o.fcb, I->h, s); }

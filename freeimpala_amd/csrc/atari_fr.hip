@@ -357,6 +357,224 @@ int conv1_wgrad_fr_launch(const uint8_t* frames, const __bf16* da1, float* slab,
 
 
 // =====================================================================================
+// Frame-resident forward of conv2 (4x4/2, 32 -> 64) and conv3 (3x3/1, 64 -> 64).
+// 8 waves: wave w owns output channels 16*(w&3)..+16 (its weight slice stays in registers as
+// the MFMA A operand, so D = [channel][pixel] and a lane ends with 4 consecutive channels
+// of one pixel) and half of the frame's 16-pixel tiles. The input frame arrives by LDS-DMA
+// in a "chunk-planar" image: plane c holds the c-th 16-byte channel chunk of every pixel,
+// so the 16 lanes of an MFMA B-fragment read (16 consecutive output pixels, same chunk)
+// hit 16 consecutive LDS slots -- conflict-free. conv2 (stride 2) additionally splits each
+// plane into even then odd input pixels, which makes its stride-2 reads consecutive too.
+// Outputs (+bias, ReLU, bf16) are staged as [pixel][64] with the 16-byte chunk index
+// XOR-swizzled by the pixel, then leave as coalesced 16-byte stores.
+// =====================================================================================
+namespace f2 {
+constexpr int NPIX = 400, PLANES = 4;        // a1: 20x20 pixels, 4 chunks of 8 channels
+constexpr int XB = NPIX * PLANES * 16;       // 25,600
+constexpr int NX = XB / 1024;                // 25 pieces
+constexpr int OUTT = 81 * 128;               // a2 tile [81][64] bf16 (swizzled chunks)
+constexpr int OUT_CH = 81 * 8;               // 648
+}  // namespace f2
+namespace f3 {
+constexpr int NPIX = 81, PLANES = 8;         // a2: 9x9 pixels, 8 chunks of 8 channels
+constexpr int XB = 11 * 1024;                // 648 slots = 10,368 B, 11 pieces (tail reads zeros)
+constexpr int NX = 11;
+constexpr int OUTT = 49 * 128;               // a3 tile [49][64] bf16 (swizzled chunks)
+constexpr int OUT_CH = 49 * 8;               // 392
+}  // namespace f3
+
+// LDS slot s of the conv2 input image -> byte offset of its 16-byte chunk in the a1 frame
+__device__ __forceinline__ uint32_t f2_src(int s) {
+    const int c = s / f2::NPIX, r = s - c * f2::NPIX;
+    const int p = r < f2::NPIX / 2 ? 2 * r : 2 * (r - f2::NPIX / 2) + 1;
+    return (uint32_t)(64 * p + 16 * c);
+}
+__device__ __forceinline__ uint32_t f3_src(int s) {
+    const int c = s / f3::NPIX, p = s - c * f3::NPIX;
+    return s < f3::NPIX * f3::PLANES ? (uint32_t)(128 * p + 16 * c) : FI_OOB;
+}
+
+template <int L>  // L = 2 (conv2) or 3 (conv3)
+struct FwdGeo;
+template <>
+struct FwdGeo<2> {  // two frames per iteration: 12 pixel tiles = 4 groups x 3
+    static constexpr int XB = f2::XB, NX = f2::NX, OUTT = f2::OUTT, OUT_CH = f2::OUT_CH;
+    static constexpr int IN_BYTES = 25600, OUT_ELEMS = 5184, IN_ELEMS = 12800, KS = 16, NT = 6, OPIX = 81;
+    static constexpr int FPI = 2, RING_I = 2;
+};
+template <>
+struct FwdGeo<3> {  // one frame per iteration: 4 pixel tiles = 4 groups x 1
+    static constexpr int XB = f3::XB, NX = f3::NX, OUTT = f3::OUTT, OUT_CH = f3::OUT_CH;
+    static constexpr int IN_BYTES = 10368, OUT_ELEMS = 3136, IN_ELEMS = 5184, KS = 18, NT = 4, OPIX = 49;
+    static constexpr int FPI = 1, RING_I = 3;
+};
+
+// 8 waves = 2 channel halves (32 channels, two 16-channel A-operand tiles in registers) x 4
+// pixel-tile groups: each B fragment read from LDS feeds two MFMAs.
+template <int L>
+__global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__ x,    // NHWC input frames
+                                                      const __bf16* __restrict__ wt,   // [64][K] (ky,kx,ci)
+                                                      const float* __restrict__ bias,  // [64]
+                                                      __bf16* __restrict__ y,          // NHWC output frames
+                                                      int nframes) {
+    using G = FwdGeo<L>;
+    constexpr int K = G::KS * 32, FPI = G::FPI, RI = G::RING_I;
+    constexpr int TPW = G::NT * FPI / 4;  // pixel tiles per wave
+    __shared__ __attribute__((aligned(16))) char smem[RI * FPI * G::XB + FPI * G::OUTT + G::NX * 64 * 4];
+    const int lane = threadIdx.x & 63, tid = threadIdx.x;
+    const int w = wave_id(), chh = w >> 2, pg = w & 3;
+    const int g = lane >> 4, c16 = lane & 15;
+    const uint32_t lds0 = lds_addr(smem);
+    char* outt = smem + RI * FPI * G::XB;
+    uint32_t* srcs = (uint32_t*)(smem + RI * FPI * G::XB + FPI * G::OUTT);  // DMA gather table
+    for (int i = tid; i < G::NX * 64; i += 512) srcs[i] = L == 2 ? f2_src(i) : f3_src(i);
+
+    // A operand (weights): lane holds W[co = 32chh + 16ct + c16][k = 32ks + 8g..+8], ct = 0, 1
+    bf16x8 wa[2][G::KS];
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+        for (int ks = 0; ks < G::KS; ++ks)
+            wa[ct][ks] = *(const bf16x8*)(wt + (size_t)(32 * chh + 16 * ct + c16) * K + 32 * ks + 8 * g);
+    float bch[2][4];
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bch[ct][r] = bias[32 * chh + 16 * ct + 4 * g + r];
+    // this wave's pixel tiles: global tile t = TPW*pg + i over the FPI frames of an iteration
+    int bbase[TPW];
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) {
+        const int t = TPW * pg + i, fi = t / G::NT, tt = t - fi * G::NT;
+        const int n = min(16 * tt + c16, G::OPIX - 1);
+        if (L == 2) {
+            const int oy = n / 9, ox = n - 9 * oy;  // input pixel (2oy+ky, 2ox+kx), even/odd split
+            bbase[i] = fi * G::XB + 16 * (f2::NPIX * g + 20 * oy + ox);
+        } else {
+            const int oy = n / 7, ox = n - 7 * oy;  // input pixel (oy+ky, ox+kx)
+            bbase[i] = fi * G::XB + 16 * (f3::NPIX * g + 9 * oy + ox);
+        }
+    }
+    __syncthreads();  // gather table ready
+
+    const int npw = (G::NX - w + 7) / 8;  // pieces per frame issued by this wave
+    const int nmine = nframes > (int)blockIdx.x ? (nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+    const int niter = (nmine + FPI - 1) / FPI;
+    // queue the frames of iteration i2 into ring slot (i2 % RI); returns the pieces issued
+    auto issue = [&](int i2) {
+        int n = 0;
+#pragma unroll
+        for (int u = 0; u < FPI; ++u) {
+            const int k = FPI * i2 + u;
+            if (k < nmine) {
+                const int f = blockIdx.x + k * gridDim.x;
+                const fi_i32x4 xr = make_rsrc(x + (size_t)f * G::IN_ELEMS, G::IN_BYTES);
+                const uint32_t slot_lds = lds0 + ((i2 % RI) * FPI + u) * G::XB;
+#pragma unroll
+                for (int i = 0; i < (G::NX + 7) / 8; ++i) {
+                    const int j = w + 8 * i;
+                    if (j < G::NX) blds16(xr, srcs[64 * j + lane], slot_lds + 1024 * j);
+                }
+                n += npw;
+            }
+        }
+        return n;
+    };
+    int issued = 0, mk[RI];
+#pragma unroll
+    for (int i = 0; i < RI; ++i) {
+        if (i < niter) issued += issue(i);
+        mk[i] = issued;
+    }
+    for (int it = 0; it < niter; ++it) {
+        const char* X = smem + (it % RI) * FPI * G::XB;
+        wait_vmcnt(issued - mk[0]);
+        lds_barrier();  // frames landed; previous out tiles drained
+        f32x4 acc[TPW][2];
+#pragma unroll
+        for (int i = 0; i < TPW; ++i) { acc[i][0] = f32x4{}; acc[i][1] = f32x4{}; }
+#pragma unroll
+        for (int ks = 0; ks < G::KS; ++ks) {
+            int imm;
+            if (L == 2) {  // tap = ks (32 channels); kx parity selects the odd-pixel half
+                const int ky = ks >> 2, kx = ks & 3;
+                imm = 16 * (10 * ky + (kx >> 1) + (f2::NPIX / 2) * (kx & 1));
+            } else {       // tap = ks/2, channel half ks&1 -> planes 4(ks&1) + g
+                const int tap = ks >> 1, ky = tap / 3, kx = tap - 3 * ky;
+                imm = 16 * (f3::NPIX * 4 * (ks & 1) + 9 * ky + kx);
+            }
+#pragma unroll
+            for (int i = 0; i < TPW; ++i) {
+                const bf16x8 b = *(const bf16x8*)(X + bbase[i] + imm);
+                acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[0][ks], b, acc[i][0], 0, 0, 0);
+                acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[1][ks], b, acc[i][1], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < TPW; ++i) {
+            const int t = TPW * pg + i, fi = t / G::NT, tt = t - fi * G::NT;
+            const int n = 16 * tt + c16;
+            if (n < G::OPIX) {
+#pragma unroll
+                for (int ct = 0; ct < 2; ++ct) {
+                    bf16x4 o;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) o[r] = (__bf16)fmaxf(acc[i][ct][r] + bch[ct][r], 0.f);
+                    const int chunk = (4 * chh + 2 * ct + (g >> 1)) ^ (n & 7);
+                    *(bf16x4*)(outt + fi * G::OUTT + 128 * n + 16 * chunk + 8 * (g & 1)) = o;
+                }
+            }
+        }
+        lds_barrier();  // out tiles complete
+        {
+#pragma unroll
+            for (int u = 0; u < FPI; ++u) {
+                const int k = FPI * it + u;
+                if (k < nmine) {
+                    u32x4* dst = (u32x4*)(y + (size_t)(blockIdx.x + k * gridDim.x) * G::OUT_ELEMS);
+#pragma unroll
+                    for (int i = 0; i < (G::OUT_CH + 511) / 512; ++i) {
+                        const int P = tid + 512 * i;
+                        if (P < G::OUT_CH) {
+                            const int n = P >> 3, c = P & 7;
+                            FI_ST16(*(const u32x4*)(outt + u * G::OUTT + 128 * n + 16 * (c ^ (n & 7))), dst + P);
+                        }
+                    }
+                }
+            }
+        }
+        lds_barrier();  // ring slot consumed
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stores drain before the next DMA
+        int mnew = issued;
+        if (it + RI < niter) {
+            issued += issue(it + RI);
+            mnew = issued;
+        }
+        // (the stores were drained, so only DMA pieces are counted)
+#pragma unroll
+        for (int i = 0; i + 1 < RI; ++i) mk[i] = mk[i + 1];
+        mk[RI - 1] = mnew;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+int conv2_fwd_fr_launch(const __bf16* a1, const __bf16* w2t, const float* bias, __bf16* a2, int nframes,
+                        int grid, hipStream_t s) {
+    hipLaunchKernelGGL(conv_fwd_fr<2>, dim3(grid), dim3(512), 0, s, a1, w2t, bias, a2, nframes);
+    FI_HIP_CHECK(hipGetLastError());
+    st_report("conv2_fwd");
+    return FI_OK;
+}
+
+int conv3_fwd_fr_launch(const __bf16* a2, const __bf16* w3t, const float* bias, __bf16* a3, int nframes,
+                        int grid, hipStream_t s) {
+    hipLaunchKernelGGL(conv_fwd_fr<3>, dim3(grid), dim3(512), 0, s, a2, w3t, bias, a3, nframes);
+    FI_HIP_CHECK(hipGetLastError());
+    st_report("conv3_fwd");
+    return FI_OK;
+}
+
+// =====================================================================================
 // Fused, frame-resident conv backward kernels (dgrad + wgrad + bias of one layer).
 // Per frame, LDS holds the layer input X (= ReLU mask of the data gradient) and the
 // upstream gradient dY; the kernel writes dX = (X > 0) * dgrad(dY, W) once and keeps
