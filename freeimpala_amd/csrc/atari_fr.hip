@@ -458,6 +458,8 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
     __syncthreads();  // gather table ready
 
     const int npw = (G::NX - w + 7) / 8;  // pieces per frame issued by this wave
+    // copy-out store instructions per frame issued by this wave (lower bound: safe to count)
+    const int nst = G::OUT_CH / 512 + (G::OUT_CH % 512 > 64 * w ? 1 : 0);
     const int nmine = nframes > (int)blockIdx.x ? (nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
     const int niter = (nmine + FPI - 1) / FPI;
     // queue the frames of iteration i2 into ring slot (i2 % RI); returns the pieces issued
@@ -480,6 +482,8 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
         }
         return n;
     };
+    ST_DECL
+    ST();
     int issued = 0, mk[RI];
 #pragma unroll
     for (int i = 0; i < RI; ++i) {
@@ -490,6 +494,7 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
         const char* X = smem + (it % RI) * FPI * G::XB;
         wait_vmcnt(issued - mk[0]);
         lds_barrier();  // frames landed; previous out tiles drained
+        if (it < 5) ST();
         f32x4 acc[TPW][2];
 #pragma unroll
         for (int i = 0; i < TPW; ++i) { acc[i][0] = f32x4{}; acc[i][1] = f32x4{}; }
@@ -510,6 +515,7 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
                 acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[1][ks], b, acc[i][1], 0, 0, 0);
             }
         }
+        if (it < 5) ST();
 #pragma unroll
         for (int i = 0; i < TPW; ++i) {
             const int t = TPW * pg + i, fi = t / G::NT, tt = t - fi * G::NT;
@@ -526,11 +532,13 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
             }
         }
         lds_barrier();  // out tiles complete
+        if (it < 5) ST();
         {
 #pragma unroll
             for (int u = 0; u < FPI; ++u) {
                 const int k = FPI * it + u;
                 if (k < nmine) {
+                    issued += nst;
                     u32x4* dst = (u32x4*)(y + (size_t)(blockIdx.x + k * gridDim.x) * G::OUT_ELEMS);
 #pragma unroll
                     for (int i = 0; i < (G::OUT_CH + 511) / 512; ++i) {
@@ -544,18 +552,20 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
             }
         }
         lds_barrier();  // ring slot consumed
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stores drain before the next DMA
-        int mnew = issued;
+        if (it < 5) ST();
+        int mnew = issued;  // (a later wait on this mark never waits for the stores above)
         if (it + RI < niter) {
             issued += issue(it + RI);
             mnew = issued;
         }
-        // (the stores were drained, so only DMA pieces are counted)
 #pragma unroll
         for (int i = 0; i + 1 < RI; ++i) mk[i] = mk[i + 1];
         mk[RI - 1] = mnew;
+        if (it < 5) ST();
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ST();
+    ST_FLUSH();
 }
 
 int conv2_fwd_fr_launch(const __bf16* a1, const __bf16* w2t, const float* bias, __bf16* a2, int nframes,
