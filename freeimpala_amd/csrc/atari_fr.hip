@@ -660,6 +660,8 @@ __device__ __forceinline__ void c2_frames(const C2Ctx& c, char* smem, Work&& wor
     const int npw = (c2::NX + c2::NDY - w + 7) / 8;  // 6 or 5 pieces per wave
     const int nst = w == 0 ? 4 : 3;                  // copy-out stores issued (lower bound)
     const int nmine = c.nframes > (int)blockIdx.x ? (c.nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+    ST_DECL
+    ST();
     int issued = 0, m0 = 0, m1 = 0, m2 = 0;
     for (int i = 0; i < 3 && i < nmine; ++i) {
         c2_issue8(c, dyo, blockIdx.x + i * gridDim.x, lds0 + i * c2::SLOT, w, lane);
@@ -672,8 +674,11 @@ __device__ __forceinline__ void c2_frames(const C2Ctx& c, char* smem, Work&& wor
         char* X = smem + slot * c2::SLOT;
         wait_vmcnt(issued - m0);
         lds_barrier();  // frame landed
+        if (it < 5) ST();
         work(X);
+        if (it < 5) ST();
         lds_barrier();  // dgrad tile complete
+        if (it < 5) ST();
         {  // da1 = (X > 0) * dX in NHWC order: chunk P = pixel P/4, channels 8*(P%4)..+8
             u32x4* dst = (u32x4*)(c.da1 + (size_t)f * 12800);
 #pragma unroll
@@ -694,11 +699,14 @@ __device__ __forceinline__ void c2_frames(const C2Ctx& c, char* smem, Work&& wor
             issued += nst;
         }
         lds_barrier();  // slot fully consumed
+        if (it < 5) ST();
         int m3 = 0;
         if (it + 3 < nmine) {
             // the previous frame's copy-out stores drain before the next DMA pieces queue
             // behind them (measured: slightly faster than letting them overlap)
+#ifndef FI_NO_DRAIN
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
             c2_issue8(c, dyo, blockIdx.x + (it + 3) * gridDim.x, lds0 + slot * c2::SLOT, w, lane);
             issued += npw;
             m3 = issued;
@@ -708,6 +716,8 @@ __device__ __forceinline__ void c2_frames(const C2Ctx& c, char* smem, Work&& wor
         m2 = m3;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ST();
+    ST_FLUSH();
 }
 
 __global__ __launch_bounds__(512, 2) void conv2_bwd_fr(const __bf16* __restrict__ a1,
@@ -883,6 +893,8 @@ __device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, Work&& wor
     const int npw = (c3::NX + c3::NDY + c3::NM - w + 7) / 8;  // 5 or 4 pieces per wave
     const int nst = w <= 2 ? 2 : 1;                           // copy-out stores issued (lower bound)
     const int nmine = c.nframes > (int)blockIdx.x ? (c.nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+    ST_DECL
+    ST();
     int issued = 0, m0 = 0, m1 = 0, m2 = 0;
     for (int i = 0; i < 3 && i < nmine; ++i) {
         c3_issue8(c, dyo, blockIdx.x + i * gridDim.x, lds0 + i * c3::SLOT, w, lane);
@@ -895,6 +907,7 @@ __device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, Work&& wor
         char* X = smem + slot * c3::SLOT;
         wait_vmcnt(issued - m0);
         lds_barrier();  // frame landed
+        if (it < 5) ST();
         if (tid < 392) {  // ReLU mask of the upstream gradient: dY *= (a3 > 0)
             const int p = tid >> 3, ch = tid & 7, py = p / 7, px = p - 7 * py;
             bf16x8* dyp = (bf16x8*)(X + c3::XB + DP * ((py + 2) * 11 + px + 2) + 16 * ch);
@@ -906,14 +919,17 @@ __device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, Work&& wor
         }
         lds_barrier();  // masked dY visible
         work(X);
+        if (it < 5) ST();
         lds_barrier();  // dgrad tile complete
+        if (it < 5) ST();
         {
             u32x4* dst = (u32x4*)(c.da2 + (size_t)f * 5184);
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 const int P = tid + 512 * i;
                 if (P < c3::OUT_CH) {
-                    const bf16x8 v = *(const bf16x8*)(outt + 8 * P);
+                    const int n = P >> 3, ch = P & 7;  // tile chunks are XOR-swizzled by pixel
+                    const bf16x8 v = *(const bf16x8*)(outt + 64 * n + 8 * (ch ^ (n & 7)));
                     const bf16x8 m = *(const bf16x8*)(X + 16 * P);
                     bf16x8 o;
 #pragma unroll
@@ -924,11 +940,14 @@ __device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, Work&& wor
             issued += nst;
         }
         lds_barrier();  // slot fully consumed
+        if (it < 5) ST();
         int m3 = 0;
         if (it + 3 < nmine) {
             // the previous frame's copy-out stores drain before the next DMA pieces queue
             // behind them (measured: slightly faster than letting them overlap)
+#ifndef FI_NO_DRAIN
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
             c3_issue8(c, dyo, blockIdx.x + (it + 3) * gridDim.x, lds0 + slot * c3::SLOT, w, lane);
             issued += npw;
             m3 = issued;
@@ -938,6 +957,8 @@ __device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, Work&& wor
         m2 = m3;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ST();
+    ST_FLUSH();
 }
 
 __global__ __launch_bounds__(512, 2) void conv3_bwd_fr(const __bf16* __restrict__ a2,
@@ -1022,40 +1043,53 @@ __global__ __launch_bounds__(512, 2) void conv3_bwd_fr(const __bf16* __restrict_
             }
         }
     } else {
-        // ---------------- data gradient (16x16x32): input channels 16wr..+16, all 6 row tiles
+        // ---------------- data gradient (16x16x32), transposed: D[ci][pixel] = W^T dYcol^T with the
+        // W slice as the register-resident A operand. Wave wr: channel tiles 2(wr&1), 2(wr&1)+1
+        // (32 channels), pixel tiles 3(wr>>1)..+2 -- each dY fragment read feeds two MFMAs, and a
+        // lane ends with 4 consecutive channels of one pixel (one 8-byte store).
         __bf16* outt = (__bf16*)(smem + c3::RING * c3::SLOT);
-        s16x8 bw[18];  // lane holds W[k = 32ks + 8g + j][ci = 16wr + (lane&15)]
+        const int chh = wr & 1, ph = wr >> 1;
+        s16x8 bw[2][18];  // lane holds W[k = 32ks + 8g + j][ci = 32chh + 16ct + (lane&15)]
 #pragma unroll
-        for (int ks = 0; ks < 18; ++ks)
-            bw[ks] = *(const s16x8*)(w3d + (size_t)(16 * wr + (lane & 15)) * 576 + 32 * ks + 8 * g);
-        int bd[6];
+        for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
-        for (int rt = 0; rt < 6; ++rt) {
-            const int pix = min(rt * 16 + (lane & 15), 80), iy = pix / 9, ix = pix - 9 * iy;
-            bd[rt] = c3::XB + DP * ((iy + 2) * 11 + ix + 2 - 24) + 16 * g;
+            for (int ks = 0; ks < 18; ++ks)
+                bw[ct][ks] = *(const s16x8*)(w3d + (size_t)(32 * chh + 16 * ct + (lane & 15)) * 576 + 32 * ks + 8 * g);
+        int bd[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const int pix = min((3 * ph + i) * 16 + (lane & 15), 80), iy = pix / 9, ix = pix - 9 * iy;
+            bd[i] = c3::XB + DP * ((iy + 2) * 11 + ix + 2 - 24) + 16 * g;
         }
         c3_frames(ctx, smem, [&](const char* X) {
+            f32x4 acc[3][2];
 #pragma unroll
-            for (int rp = 0; rp < 3; ++rp) {
-                f32x4 acc0 = {}, acc1 = {};
-                const char* base0 = X + bd[2 * rp];
-                const char* base1 = X + bd[2 * rp + 1];
+            for (int i = 0; i < 3; ++i) { acc[i][0] = f32x4{}; acc[i][1] = f32x4{}; }
 #pragma unroll
-                for (int ks = 0; ks < 18; ++ks) {
-                    const int tap = ks >> 1, ky = tap / 3, kx = tap - 3 * ky;
-                    const int off = DP * (24 - (11 * ky + kx)) + 64 * (ks & 1);
-                    const s16x8 a0 = *(const s16x8*)(base0 + off);
-                    const s16x8 a1 = *(const s16x8*)(base1 + off);
-                    acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a0),
-                                                                  __builtin_bit_cast(bf16x8, bw[ks]), acc0, 0, 0, 0);
-                    acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a1),
-                                                                  __builtin_bit_cast(bf16x8, bw[ks]), acc1, 0, 0, 0);
+            for (int ks = 0; ks < 18; ++ks) {
+                const int tap = ks >> 1, ky = tap / 3, kx = tap - 3 * ky;
+                const int off = DP * (24 - (11 * ky + kx)) + 64 * (ks & 1);
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    const bf16x8 b = __builtin_bit_cast(bf16x8, *(const s16x8*)(X + bd[i] + off));
+                    acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bw[0][ks]), b,
+                                                                       acc[i][0], 0, 0, 0);
+                    acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bw[1][ks]), b,
+                                                                       acc[i][1], 0, 0, 0);
                 }
+            }
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int row = rp * 32 + 4 * g + r;
-                    outt[row * 64 + 16 * wr + (lane & 15)] = (__bf16)acc0[r];
-                    if (row + 16 < 81) outt[(row + 16) * 64 + 16 * wr + (lane & 15)] = (__bf16)acc1[r];
+            for (int i = 0; i < 3; ++i) {
+                const int pix = (3 * ph + i) * 16 + (lane & 15);
+                if (pix < 81) {
+#pragma unroll
+                    for (int ct = 0; ct < 2; ++ct) {
+                        bf16x4 o;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) o[r] = (__bf16)acc[i][ct][r];
+                        const int chunk = (4 * chh + 2 * ct + (g >> 1)) ^ (pix & 7);
+                        *(bf16x4*)((char*)outt + 128 * pix + 16 * chunk + 8 * (g & 1)) = o;
+                    }
                 }
             }
         });
