@@ -30,18 +30,19 @@ MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}  # dense peaks (no sparsity)
 
 
 def kernel_work(arch, T, B, A, D=128, H=256):
-    """Algorithmic work per launch for each tagged kernel site: (kind, amount).
-    kind 'flop' (MFMA-bound GEMMs) or 'byte' (HBM-bound). See DESIGN.md section 5."""
+    """Algorithmic work per launch for each tagged kernel site: (flops, bytes).
+    The roofline bound is whichever of MFMA or HBM time at peak is larger."""
     R = (T + 1) * B
     TB = T * B
-    w = {"vtrace": ("byte", (12 * A + 28) * TB)}
+    w = {"vtrace": (0, (12 * A + 28) * TB)}
     if arch == "mlp":
         O = A + 1
+        f32 = 4
         w.update({
-            "mlp_fwd_l1": ("flop", 2 * R * D * H), "mlp_fwd_l2": ("flop", 2 * R * H * H),
-            "mlp_fwd_heads": ("flop", 2 * R * H * O), "mlp_wgrad_heads": ("flop", 2 * R * H * O),
-            "mlp_dgrad_heads": ("flop", 2 * R * O * H), "mlp_wgrad_l2": ("flop", 2 * R * H * H),
-            "mlp_dgrad_l2": ("flop", 2 * R * H * H), "mlp_wgrad_l1": ("flop", 2 * R * D * H),
+            "mlp_fwd_l1": (2 * R * D * H, R * f32 * (D + H)), "mlp_fwd_l2": (2 * R * H * H, R * f32 * 2 * H),
+            "mlp_fwd_heads": (2 * R * H * O, R * f32 * (H + O)), "mlp_wgrad_heads": (2 * R * H * O, R * f32 * (H + O)),
+            "mlp_dgrad_heads": (2 * R * O * H, R * f32 * (O + 2 * H)), "mlp_wgrad_l2": (2 * R * H * H, R * f32 * 2 * H),
+            "mlp_dgrad_l2": (2 * R * H * H, R * f32 * 3 * H), "mlp_wgrad_l1": (2 * R * D * H, R * f32 * (D + H)),
         })
     else:
         from freeimpala_amd.atari_shapes import atari_kernel_work
@@ -207,20 +208,21 @@ def main():
     def roof(name, ms=None):
         if name not in kt or name not in work:
             return None
-        kind, amount = work[name]
+        flops, nbytes = work[name]
         ms = kt[name]["ms"] if ms is None else ms
         tr = traffic.get(name)
-        if kind == "byte":
-            ach = amount / (ms * 1e-3) / 1e9
-            return {"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": tr,
-                    "algorithmic_per_launch": amount, "launch_ms": round(ms, 5)}
-        ach = amount / (ms * 1e-3) / 1e12
-        peak = MFMA_PEAK_TFLOPS[dtype]
-        return {"kernel": name, "bound": "mfma", "achieved": round(ach, 2), "peak": peak,
-                "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": tr,
-                "traffic_unit": "HBM bytes per launch (rocprofv3 PMC)" if tr else None,
-                "algorithmic_per_launch": amount, "launch_ms": round(ms, 5)}
+        peak_f = MFMA_PEAK_TFLOPS[dtype] * 1e12
+        t_mfma, t_hbm = flops / peak_f, nbytes / (HBM_PEAK_GBS * 1e9)
+        common = {"kernel": name, "traffic": tr, "launch_ms": round(ms, 5),
+                  "algorithmic_flops": flops, "algorithmic_bytes": nbytes,
+                  "time_at_peak_ms": {"mfma": round(t_mfma * 1e3, 4), "hbm": round(t_hbm * 1e3, 4)}}
+        if t_hbm >= t_mfma:
+            ach = nbytes / (ms * 1e-3) / 1e9
+            return dict(common, bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                        frac=round(ach / HBM_PEAK_GBS, 4))
+        ach = flops / (ms * 1e-3) / 1e12
+        return dict(common, bound="mfma", achieved=round(ach, 2), peak=MFMA_PEAK_TFLOPS[dtype],
+                    unit="TFLOP/s", frac=round(ach / MFMA_PEAK_TFLOPS[dtype], 4))
 
     result = {
         "metric": METRIC, "value": round(value, 1), "unit": "env-steps/s", "n_gpus": N,
