@@ -74,7 +74,6 @@ constexpr int PLANE = 84 * 21 * 16 + 64;            // bytes (+64: plane 1 shift
 constexpr int IMG = 2 * PLANE;                      // 56,576 B
 constexpr int OUT = 400 * 32 * 2;                   // 25,600 B output / dY tile
 constexpr int OUT_CH = OUT / 16;                    // 1600 16-byte chunks
-constexpr int OUT_PER_T = (OUT_CH + 255) / 256;     // 7
 }  // namespace c1
 
 __device__ __forceinline__ void u8x16_to_bf16(u32x4 v, bf16x8& lo, bf16x8& hi) {
@@ -243,100 +242,103 @@ __device__ __forceinline__ bf16x8 tr2(const char* p0, const char* p1) {
     return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-__global__ __launch_bounds__(256, 1) void conv1_wgrad_fr(const uint8_t* __restrict__ frames,
+// 8 waves, wave w = k-tile w (kernel row ky = w: 8 taps x 4 channels = 32 k) for all 32
+// output channels. Per frame: the raw u8 frame (1 slot, prefetched one frame ahead) and the
+// da1 tile (2-slot ring, two frames ahead) arrive by LDS-DMA; the frame is converted once
+// into the bf16 pair-plane image; both MFMA operands come from transposed LDS reads.
+__global__ __launch_bounds__(512, 2) void conv1_wgrad_fr(const uint8_t* __restrict__ frames,
                                                          const __bf16* __restrict__ da1,
                                                          float* __restrict__ slab,
                                                          float* __restrict__ cs_slab, int nframes) {
-    __shared__ __attribute__((aligned(16))) char smem[c1::IMG + c1::OUT];
-    char* img = smem;
-    char* dy = smem + c1::IMG;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    __shared__ __attribute__((aligned(16))) char smem[c1::RAW + 2 * c1::OUT + c1::IMG];
+    char* raw = smem;
+    char* img = smem + c1::RAW + 2 * c1::OUT;
+    const uint32_t lds0 = lds_addr(smem);
+    const int lane = threadIdx.x & 63, w = wave_id(), tid = threadIdx.x;
     const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-    // per-lane tr-read column: k = k0 + 16*(g&1) + 4p, i.e. tap = k0/4 + 4*(g&1) + p
-    f32x16 acc0 = {}, acc1 = {};
-    float csum[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // bias grad partial: co = 8*(chunk%4) + j
-
-    u32x4 pre[c1::PER_T], pdy[c1::OUT_PER_T];
-    auto fetch = [&](int ff) {
-        c1_fetch_frame(frames + (size_t)ff * 28224, pre);
-        const u32x4* s = (const u32x4*)(da1 + (size_t)ff * 12800);
+    // lane's tr column: k = 32w + 16(g&1) + 4p = tap (ky = w, kx = 4(g&1) + p) x 4 channels
+    const int toff = w * 84 + 4 * (g & 1) + p;  // pixel offset of the tap relative to (4oy, 4ox)
+    int wao[25][2];  // image offset of the A^T (im2col) transposed read, per m-step / half
 #pragma unroll
-        for (int i = 0; i < c1::OUT_PER_T; ++i) {
-            const int c = threadIdx.x + 256 * i;
-            pdy[i] = c < c1::OUT_CH ? __builtin_nontemporal_load(s + c) : u32x4{0, 0, 0, 0};
-        }
-    };
-    // tap geometry of this lane for the two k-tiles of this wave (k0 = 64w + 32t)
-    int toff[2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-        const int tap = (64 * w + 32 * t) / 4 + 4 * (g & 1) + p;
-        const int ky = tap >> 3, kx = tap & 7;
-        toff[t] = ky * 84 + kx;  // pixel offset of the tap relative to (4oy, 4ox)
-    }
-    // frame-invariant per-lane LDS offsets of every transposed read: A [ms][t][lo/hi], B [ms][lo/hi]
-    int wao[25][2][2], wbo[25][2];
-#pragma unroll
-    for (int ms = 0; ms < 25; ++ms) {
-        const int m_lo = ms * 16 + 8 * (g >> 1) + q;
+    for (int ms = 0; ms < 25; ++ms)
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
-            const int m = m_lo + 4 * hh;
+            const int m = ms * 16 + 8 * (g >> 1) + q + 4 * hh;
             const int oy = m / 20, ox = m - oy * 20;
-            wbo[ms][hh] = m * 64 + (16 * (g & 1) + 4 * p) * 2;
+            const int P = oy * 4 * 84 + ox * 4 + toff;
+            const int y = P / 84, x = P - y * 84;
+            wao[ms][hh] = ((x >> 1) & 1) * c1::PLANE + 16 * (y * 21 + (x >> 2)) + 8 * (x & 1);
+        }
+    // da1 tile [m][32 co]: B read of rows m = 16ms + 8(g>>1) + q + 4hh -> base_hh + 1024 ms
+    const int wb0 = (8 * (g >> 1) + q) * 64 + (16 * (g & 1) + 4 * p) * 2, wb1 = wb0 + 4 * 64;
+    f32x16 acc = {};
+    float bsum = 0.f;
+
+    const int nmine = nframes > (int)blockIdx.x ? (nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+    auto issue_raw = [&](int k) {
+        const fi_i32x4 rr = make_rsrc(frames + (size_t)(blockIdx.x + k * gridDim.x) * 28224, 28224);
 #pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                const int P = oy * 4 * 84 + ox * 4 + toff[t];
-                const int y = P / 84, x = P - y * 84;
-                wao[ms][t][hh] = ((x >> 1) & 1) * c1::PLANE + 16 * (y * 21 + (x >> 2)) + 8 * (x & 1);
+        for (int i = 0; i < 4; ++i) {
+            const int j = w + 8 * i;
+            if (j < 28) blds16(rr, 16 * lane + 1024 * j, lds0 + 1024 * j);
+        }
+        return w < 4 ? 4 : 3;
+    };
+    auto issue_dy = [&](int k) {
+        const fi_i32x4 dr = make_rsrc(da1 + (size_t)(blockIdx.x + k * gridDim.x) * 12800, 25600);
+        const uint32_t base = lds0 + c1::RAW + (k & 1) * c1::OUT;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int j = w + 8 * i;
+            if (j < 25) blds16(dr, 16 * lane + 1024 * j, base + 1024 * j);
+        }
+        return w == 0 ? 4 : 3;
+    };
+    int issued = 0, mark = 0;
+    if (nmine > 0) { issued += issue_raw(0); issued += issue_dy(0); }
+    mark = issued;
+    if (nmine > 1) issued += issue_dy(1);
+    for (int it = 0; it < nmine; ++it) {
+        const char* dy = smem + c1::RAW + (it & 1) * c1::OUT;
+        wait_vmcnt(issued - mark);
+        lds_barrier();  // raw frame + da1 tile landed; image free
+#pragma unroll
+        for (int i = 0; i < (c1::FRAME_LOADS + 511) / 512; ++i) {
+            const int u = tid + 512 * i;
+            if (u < c1::FRAME_LOADS) {
+                bf16x8 lo, hi;
+                u8x16_to_bf16(*(const u32x4*)(raw + 16 * u), lo, hi);
+                *(bf16x8*)(img + 16 * u) = lo;
+                *(bf16x8*)(img + c1::PLANE + 16 * u) = hi;
             }
         }
-    }
-    int f = blockIdx.x;
-    if (f < nframes) fetch(f);
-    for (; f < nframes; f += gridDim.x) {
-        c1_store_image(img, pre);
-#pragma unroll
-        for (int i = 0; i < c1::OUT_PER_T; ++i) {
-            const int c = threadIdx.x + 256 * i;
-            if (c < c1::OUT_CH) {
-                *(u32x4*)(dy + 16 * c) = pdy[i];
-                const bf16x8 v = __builtin_bit_cast(bf16x8, pdy[i]);
-#pragma unroll
-                for (int j = 0; j < 8; ++j) csum[j] += (float)v[j];
-            }
-        }
-        const int fn = f + gridDim.x;
-        if (fn < nframes) fetch(fn);
-        __syncthreads();
+        lds_barrier();  // image ready; raw slot free
+        if (it + 1 < nmine) issued += issue_raw(it + 1);
+        mark = issued;
 #pragma unroll
         for (int ms = 0; ms < 25; ++ms) {
-            const bf16x8 bfr = tr2(dy + wbo[ms][0], dy + wbo[ms][1]);
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr2(img + wao[ms][0][0], img + wao[ms][0][1]), bfr, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr2(img + wao[ms][1][0], img + wao[ms][1][1]), bfr, acc1, 0, 0, 0);
+            const bf16x8 bfr = tr2(dy + wb0 + 1024 * ms, dy + wb1 + 1024 * ms);
+            if (w == 0) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) bsum += (float)bfr[j];
+            }
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr2(img + wao[ms][0], img + wao[ms][1]), bfr, acc, 0, 0, 0);
         }
-        __syncthreads();
+        lds_barrier();  // image and da1 slot consumed
+        if (it + 2 < nmine) issued += issue_dy(it + 2);
     }
-    // partial slab: rows k = 64w + 32t + (r&3) + 8(r>>2) + 4(lane>>5), col co = lane&31
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // partial slab: rows k = 32w + (r&3) + 8(r>>2) + 4(lane>>5), col co = lane&31
     float* out = slab + (size_t)blockIdx.x * 256 * 32;
     const float inv255 = 1.0f / 255.0f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-        const int k = 64 * w + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        out[k * 32 + (lane & 31)] = acc0[r] * inv255;
-        out[(k + 32) * 32 + (lane & 31)] = acc1[r] * inv255;
+        const int k = 32 * w + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        out[k * 32 + (lane & 31)] = acc[r] * inv255;
     }
-    // bias partial: thread's chunks all have co octet = (threadIdx.x % 4) (256 % 4 == 0)
-    __syncthreads();
-    float* red = (float*)smem;  // [256][8]
-#pragma unroll
-    for (int j = 0; j < 8; ++j) red[threadIdx.x * 8 + j] = csum[j];
-    __syncthreads();
-    if (threadIdx.x < 32) {
-        const int oct = threadIdx.x >> 3, j = threadIdx.x & 7;
-        float s = 0.f;
-        for (int t = oct; t < 256; t += 4) s += red[t * 8 + j];
-        cs_slab[(size_t)blockIdx.x * 32 + threadIdx.x] = s;
+    if (w == 0) {  // lanes l and l+32: same co = 16(g&1) + 4p + ... (tr column), other m half
+        const float o = __shfl_xor(bsum, 32, 64);
+        if (lane < 32) cs_slab[(size_t)blockIdx.x * 32 + lane] = bsum + o;
     }
 }
 
@@ -350,7 +352,7 @@ int conv1_fwd_fr_launch(const uint8_t* frames, const __bf16* w1t, const float* b
 
 int conv1_wgrad_fr_launch(const uint8_t* frames, const __bf16* da1, float* slab, float* cs_slab,
                           int nframes, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(conv1_wgrad_fr, dim3(grid), dim3(256), 0, s, frames, da1, slab, cs_slab, nframes);
+    hipLaunchKernelGGL(conv1_wgrad_fr, dim3(grid), dim3(512), 0, s, frames, da1, slab, cs_slab, nframes);
     FI_HIP_CHECK(hipGetLastError());
     return FI_OK;
 }
