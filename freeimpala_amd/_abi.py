@@ -58,6 +58,11 @@ SIGNATURES = {
     "fi_learner_param_bytes": ([_P], C.c_size_t),
     "fi_learner_entry_bytes": ([_P], C.c_size_t),
     "fi_learner_step": ([_P, C.POINTER(_P), C.c_size_t, C.c_size_t, C.POINTER(StepStats)], C.c_int),
+    "fi_learner_step_async": ([_P, C.POINTER(_P), C.c_size_t, C.c_size_t], C.c_int),
+    "fi_learner_wait": ([_P, C.POINTER(StepStats)], C.c_int),
+    "fi_learner_state_bytes": ([_P], C.c_size_t),
+    "fi_learner_save_state": ([_P, _P, C.c_size_t], C.c_int),
+    "fi_learner_load_state": ([_P, _P, C.c_size_t], C.c_int),
     "fi_learner_step_resident": ([_P, C.POINTER(StepStats)], C.c_int),
     "fi_learner_synth_batch": ([_P, C.c_uint64, C.c_int32, C.c_int32], C.c_int),
     "fi_learner_get_params": ([_P, _P, C.c_size_t, C.POINTER(C.c_uint64)], C.c_int),

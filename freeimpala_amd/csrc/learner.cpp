@@ -73,8 +73,13 @@ struct fi_learner {
     size_t slab_floats = 0;
     int splits = 1;
     AtariNet* atari = nullptr;
-    // host entry staging
-    char* pinned = nullptr;
+    // host entry staging: two pinned buffers, so the host copy of batch k+1 overlaps the
+    // device step of batch k (fi_learner_step_async); each has an event marking the end of
+    // the H2D copy that reads it
+    char* pinned2[2] = {nullptr, nullptr};
+    hipEvent_t h2d_done[2] = {nullptr, nullptr};
+    int stage = 0;
+    bool in_flight = false;  // an async step was enqueued and not yet waited for
     char* rec_dev = nullptr;
     size_t rec_bytes = 0;
     size_t rec_entry_bytes = 0;
@@ -183,7 +188,10 @@ static void destroy(fi_learner* l) {
     if (l->comm) ncclCommDestroy(l->comm);
     atari_destroy(l->atari);
     for (void* p : l->allocs) hipFree(p);
-    if (l->pinned) hipHostFree(l->pinned);
+    for (int i = 0; i < 2; ++i) {
+        if (l->pinned2[i]) hipHostFree(l->pinned2[i]);
+        if (l->h2d_done[i]) hipEventDestroy(l->h2d_done[i]);
+    }
     for (auto& e : l->ev)
         if (e) hipEventDestroy(e);
     for (auto& e : l->tag_ev)
@@ -550,8 +558,9 @@ static void parallel_copy(char* dst, const void* const* entries, size_t n, size_
     for (auto& t : th) t.join();
 }
 
-extern "C" int fi_learner_step(fi_learner* l, const void* const* entries, size_t n_entries,
-                               size_t entry_bytes, fi_step_stats* out) {
+// stage M host entries (only their first T+1 records) into the next pinned buffer and
+// enqueue its H2D copy; returns once the host copy is done (the entries may then be freed)
+static int stage_entries(fi_learner* l, const void* const* entries, size_t n_entries, size_t entry_bytes) {
     FI_REQUIRE(l && entries, "step: null argument");
     FI_REQUIRE(l->cfg.arch == FI_ARCH_MLP,
                "step: host trajectory records carry <=128-float observations (MLP); the Atari "
@@ -561,31 +570,80 @@ extern "C" int fi_learner_step(fi_learner* l, const void* const* entries, size_t
     FI_REQUIRE(entry_bytes >= need, "step: entry_bytes < (T+1)*1024");
     for (size_t i = 0; i < n_entries; ++i) FI_REQUIRE(entries[i], "step: null entry");
     FI_HIP_CHECK(hipSetDevice(l->dev));
-    try {
-        const size_t bytes = n_entries * need;
-        if (bytes > l->rec_bytes) {
-            FI_HIP_CHECK(hipStreamSynchronize(l->stream));
-            if (l->pinned) hipHostFree(l->pinned);
-            if (l->rec_dev) {
-                hipFree(l->rec_dev);
-                l->allocs.erase(std::find(l->allocs.begin(), l->allocs.end(), (void*)l->rec_dev));
-            }
-            l->pinned = nullptr;
-            l->rec_dev = nullptr;
-            l->rec_bytes = 0;
-            FI_HIP_CHECK(hipHostMalloc((void**)&l->pinned, bytes, hipHostMallocDefault));
-            FI_TRY(dalloc(l, (void**)&l->rec_dev, bytes));
-            l->rec_bytes = bytes;
+    const size_t bytes = n_entries * need;
+    if (bytes > l->rec_bytes) {
+        FI_HIP_CHECK(hipStreamSynchronize(l->stream));
+        for (int i = 0; i < 2; ++i) {
+            if (l->pinned2[i]) hipHostFree(l->pinned2[i]);
+            l->pinned2[i] = nullptr;
         }
-        // only the first (T+1) records of each entry are read; they are packed at stride `need`
-        FI_HIP_CHECK(hipStreamSynchronize(l->stream));  // pinned buffer reuse
-        parallel_copy(l->pinned, entries, n_entries, need, need);
-        FI_HIP_CHECK(hipMemcpyAsync(l->rec_dev, l->pinned, bytes, hipMemcpyHostToDevice, l->stream));
-        l->rec_entry_bytes = need;
+        if (l->rec_dev) {
+            hipFree(l->rec_dev);
+            l->allocs.erase(std::find(l->allocs.begin(), l->allocs.end(), (void*)l->rec_dev));
+        }
+        l->rec_dev = nullptr;
+        l->rec_bytes = 0;
+        for (int i = 0; i < 2; ++i) {
+            FI_HIP_CHECK(hipHostMalloc((void**)&l->pinned2[i], bytes, hipHostMallocDefault));
+            if (!l->h2d_done[i]) FI_HIP_CHECK(hipEventCreateWithFlags(&l->h2d_done[i], hipEventDisableTiming));
+            FI_HIP_CHECK(hipEventRecord(l->h2d_done[i], l->stream));
+        }
+        FI_TRY(dalloc(l, (void**)&l->rec_dev, bytes));
+        l->rec_bytes = bytes;
+    }
+    const int s = l->stage;
+    l->stage ^= 1;
+    // the H2D that last read this pinned buffer (two steps ago) must be done before reuse
+    FI_HIP_CHECK(hipEventSynchronize(l->h2d_done[s]));
+    parallel_copy(l->pinned2[s], entries, n_entries, need, need);
+    // rec_dev is rewritten in stream order, after the previous step's ingest kernel read it
+    FI_HIP_CHECK(hipMemcpyAsync(l->rec_dev, l->pinned2[s], bytes, hipMemcpyHostToDevice, l->stream));
+    FI_HIP_CHECK(hipEventRecord(l->h2d_done[s], l->stream));
+    l->rec_entry_bytes = need;
+    return FI_OK;
+}
+
+extern "C" int fi_learner_step(fi_learner* l, const void* const* entries, size_t n_entries,
+                               size_t entry_bytes, fi_step_stats* out) {
+    try {
+        FI_TRY(stage_entries(l, entries, n_entries, entry_bytes));
+        l->in_flight = false;
         return run_step(l, true, out ? out : nullptr);
     } catch (const std::exception& e) {
         return fail(FI_ERR_STATE, std::string("step: ") + e.what());
     }
+}
+
+extern "C" int fi_learner_step_async(fi_learner* l, const void* const* entries, size_t n_entries,
+                                     size_t entry_bytes) {
+    try {
+        FI_TRY(stage_entries(l, entries, n_entries, entry_bytes));
+        FI_TRY(run_step(l, true, nullptr));  // enqueued only (no stats requested: no sync)
+        l->in_flight = true;
+        return FI_OK;
+    } catch (const std::exception& e) {
+        return fail(FI_ERR_STATE, std::string("step_async: ") + e.what());
+    }
+}
+
+extern "C" int fi_learner_wait(fi_learner* l, fi_step_stats* out) {
+    FI_REQUIRE(l, "wait: null learner");
+    FI_HIP_CHECK(hipSetDevice(l->dev));
+    FI_HIP_CHECK(hipStreamSynchronize(l->stream));
+    l->in_flight = false;
+    if (out) {
+        double h[4];
+        FI_HIP_CHECK(hipMemcpy(h, l->small, sizeof(h), hipMemcpyDeviceToHost));
+        const fi_vtrace_hparams& hp = l->cfg.hp;
+        out->pg_loss = h[0];
+        out->baseline_loss = h[1];
+        out->entropy_loss = h[2];
+        out->total_loss = h[0] + hp.baseline_cost * h[1] + hp.entropy_cost * h[2];
+        out->grad_norm = std::sqrt(h[3]);
+        out->version = l->version;
+        out->step_ms = 0.f;  // not timed on the asynchronous path
+    }
+    return FI_OK;
 }
 
 extern "C" int fi_learner_synth_batch(fi_learner* l, uint64_t seed, int32_t b_global,
@@ -655,6 +713,57 @@ extern "C" int fi_learner_set_params(fi_learner* l, const void* src, size_t byte
     if (l->atari) FI_TRY(atari_sync_weights(l->atari, l->params, l->stream));
     FI_HIP_CHECK(hipStreamSynchronize(l->stream));
     l->version = version;
+    return FI_OK;
+}
+
+// ------------------------------------------------------------------ checkpoint / resume
+// State blob: header {magic, abi, arch, nparams, step_count, version} then fp32 params, Adam
+// m, Adam v (little endian). Together with the published Model blob this lets a restarted
+// learner continue bit-identically.
+namespace {
+struct StateHeader {
+    uint32_t magic, abi;
+    int32_t arch, step_count;
+    uint64_t nparams, version;
+};
+constexpr uint32_t kStateMagic = 0x46495354u;  // "FIST"
+}  // namespace
+
+extern "C" size_t fi_learner_state_bytes(const fi_learner* l) {
+    return l ? sizeof(StateHeader) + 3 * l->nparams * sizeof(float) : 0;
+}
+
+extern "C" int fi_learner_save_state(fi_learner* l, void* dst, size_t bytes) {
+    FI_REQUIRE(l && dst, "save_state: null argument");
+    FI_REQUIRE(bytes == fi_learner_state_bytes(l), "save_state: bytes != fi_learner_state_bytes");
+    FI_HIP_CHECK(hipSetDevice(l->dev));
+    StateHeader h{kStateMagic, FI_ABI_VERSION, l->cfg.arch, l->step_count, l->nparams, l->version};
+    char* o = (char*)dst;
+    std::memcpy(o, &h, sizeof(h));
+    float* f = (float*)(o + sizeof(h));
+    FI_HIP_CHECK(hipMemcpyAsync(f, l->params, l->nparams * 4, hipMemcpyDeviceToHost, l->stream));
+    FI_HIP_CHECK(hipMemcpyAsync(f + l->nparams, l->opt_m, l->nparams * 4, hipMemcpyDeviceToHost, l->stream));
+    FI_HIP_CHECK(hipMemcpyAsync(f + 2 * l->nparams, l->opt_v, l->nparams * 4, hipMemcpyDeviceToHost, l->stream));
+    FI_HIP_CHECK(hipStreamSynchronize(l->stream));
+    return FI_OK;
+}
+
+extern "C" int fi_learner_load_state(fi_learner* l, const void* src, size_t bytes) {
+    FI_REQUIRE(l && src, "load_state: null argument");
+    FI_REQUIRE(bytes == fi_learner_state_bytes(l), "load_state: bytes != fi_learner_state_bytes");
+    StateHeader h;
+    std::memcpy(&h, src, sizeof(h));
+    FI_REQUIRE(h.magic == kStateMagic && h.abi == FI_ABI_VERSION, "load_state: not a learner state blob");
+    FI_REQUIRE(h.arch == l->cfg.arch && h.nparams == l->nparams, "load_state: state of a different network");
+    FI_HIP_CHECK(hipSetDevice(l->dev));
+    const float* f = (const float*)((const char*)src + sizeof(h));
+    FI_HIP_CHECK(hipMemcpyAsync(l->params, f, l->nparams * 4, hipMemcpyHostToDevice, l->stream));
+    FI_HIP_CHECK(hipMemcpyAsync(l->opt_m, f + l->nparams, l->nparams * 4, hipMemcpyHostToDevice, l->stream));
+    FI_HIP_CHECK(hipMemcpyAsync(l->opt_v, f + 2 * l->nparams, l->nparams * 4, hipMemcpyHostToDevice, l->stream));
+    if (l->atari) FI_TRY(atari_sync_weights(l->atari, l->params, l->stream));
+    FI_HIP_CHECK(hipStreamSynchronize(l->stream));
+    l->step_count = h.step_count;
+    l->version = h.version;
     return FI_OK;
 }
 

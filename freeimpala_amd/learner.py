@@ -61,6 +61,29 @@ class DeviceLearner:
               "fi_learner_step")
         return st.as_dict() if stats else {}
 
+    def step_async(self, batch: Sequence[bytes | bytearray | np.ndarray]) -> None:
+        """Stage the entries (copied before return) and enqueue the step; see wait()."""
+        bufs = [np.frombuffer(e, dtype=np.uint8) if not isinstance(e, np.ndarray)
+                else np.ascontiguousarray(e).view(np.uint8).ravel() for e in batch]
+        n = len(bufs)
+        eb = min(b.nbytes for b in bufs) if bufs else 0
+        ptrs = (C.c_void_p * n)(*[b.ctypes.data for b in bufs])
+        check(lib().fi_learner_step_async(self._h, ptrs, n, eb), "fi_learner_step_async")
+
+    def wait(self) -> dict:
+        st = _abi.StepStats()
+        check(lib().fi_learner_wait(self._h, C.byref(st)), "fi_learner_wait")
+        return st.as_dict()
+
+    def save_state(self) -> bytes:
+        n = lib().fi_learner_state_bytes(self._h)
+        buf = (C.c_char * n)()
+        check(lib().fi_learner_save_state(self._h, buf, n), "fi_learner_save_state")
+        return bytes(buf)
+
+    def load_state(self, blob: bytes) -> None:
+        check(lib().fi_learner_load_state(self._h, blob, len(blob)), "fi_learner_load_state")
+
     def step_resident(self, stats: bool = True) -> dict | None:
         st = _abi.StepStats()
         check(lib().fi_learner_step_resident(self._h, C.byref(st) if stats else None),

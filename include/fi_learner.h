@@ -105,12 +105,25 @@ size_t fi_learner_entry_bytes(const fi_learner* l);  /* minimum (T+1)*1024 per e
 int fi_learner_step(fi_learner* l, const void* const* entries, size_t n_entries,
                     size_t entry_bytes, fi_step_stats* out);
 int fi_learner_step_resident(fi_learner* l, fi_step_stats* out);
+/* Asynchronous form: copies the entries into one of two pinned
+ * buffers, enqueues the H2D copy and the whole step, and returns -- the caller may free the
+ * entries and read the next batch while the device works. fi_learner_wait blocks until the
+ * last enqueued step is done and reports its statistics (step_ms = 0). Publication calls
+ * (fi_learner_get_params*) also see the completed step.                                  */
+int fi_learner_step_async(fi_learner* l, const void* const* entries, size_t n_entries,
+                          size_t entry_bytes);
+int fi_learner_wait(fi_learner* l, fi_step_stats* out);
 int fi_learner_synth_batch(fi_learner* l, uint64_t seed, int32_t b_global, int32_t b_offset);
 
 /* ---- parameter publication / resume (ModelManager::updateModel, Model::loadFromDisk) - */
 int fi_learner_get_params(fi_learner* l, void* dst, size_t bytes, uint64_t* version);
 int fi_learner_get_params_fp32(fi_learner* l, float* dst, size_t count);
 int fi_learner_set_params(fi_learner* l, const void* src, size_t bytes, uint64_t version);
+/* Checkpoint / resume of the full learner state (params, Adam m and v, step count, version):
+ * Learner::checkpointModel / --starting-model with optimizer state. */
+size_t fi_learner_state_bytes(const fi_learner* l);
+int fi_learner_save_state(fi_learner* l, void* dst, size_t bytes);
+int fi_learner_load_state(fi_learner* l, const void* src, size_t bytes);
 
 /* ---- data parallel (RCCL over xGMI) ------------------------------------------------ */
 int fi_comm_unique_id_bytes(void);

@@ -168,6 +168,42 @@ public:
         return true;
     }
 
+    // Asynchronous step: returns once the batch is copied into pinned memory (the caller may
+    // drop it and block in readBatch for the next one); wait() completes it.
+    bool step_async(size_t player_index, const std::vector<std::vector<char>>& batch) {
+        if (player_index >= handles_.size()) return fail(0, "player_index out of range");
+        if (batch.empty()) return fail(player_index, "empty batch");
+        const size_t eb = batch[0].size();
+        std::vector<const void*> ptrs(batch.size());
+        for (size_t i = 0; i < batch.size(); ++i) {
+            if (batch[i].size() != eb) return fail(player_index, "entries of different sizes");
+            ptrs[i] = batch[i].data();
+        }
+        if (fi_learner_step_async(handles_[player_index], ptrs.data(), ptrs.size(), eb) != FI_OK)
+            return fail(player_index, fi_last_error());
+        return true;
+    }
+    bool wait(size_t p) {
+        if (p >= handles_.size()) return fail(0, "player_index out of range");
+        fi_step_stats st{};
+        if (fi_learner_wait(handles_[p], &st) != FI_OK) return fail(p, fi_last_error());
+        stats_[p] = st;
+        return true;
+    }
+
+    // Full learner state (params + Adam moments + counters) for checkpoint / resume.
+    bool save_state(size_t p, std::vector<char>& blob) {
+        if (p >= handles_.size()) return fail(0, "player_index out of range");
+        blob.resize(fi_learner_state_bytes(handles_[p]));
+        if (fi_learner_save_state(handles_[p], blob.data(), blob.size()) != FI_OK) return fail(p, fi_last_error());
+        return true;
+    }
+    bool load_state(size_t p, const std::vector<char>& blob) {
+        if (p >= handles_.size()) return fail(0, "player_index out of range");
+        if (fi_learner_load_state(handles_[p], blob.data(), blob.size()) != FI_OK) return fail(p, fi_last_error());
+        return true;
+    }
+
     // Parameters of player p as the published Model blob (fp32 or bf16, little endian,
     // DESIGN.md section 3 order); resizes `blob` to param_bytes().
     bool publish(size_t p, std::vector<char>& blob, uint64_t& version) {

@@ -188,3 +188,45 @@ def test_bad_arguments_fail_loudly():
         L.step([b"\0" * 1024] * 16)  # entries shorter than (T+1)*1024
     with pytest.raises(FiError):
         L.step([b"\0" * 4096] * 15)  # wrong batch size
+
+
+def test_async_step_matches_sync_steps(orc):
+    """fi_learner_step_async x2 (entries freed right after each call) then wait == two
+    synchronous steps on the same batches: same parameters, same last statistics."""
+    from freeimpala_amd.learner import pack_records
+    T, B = 6, 32
+    batches = []
+    for seed in (21, 22):
+        b = orc.synth_batch(seed, T=T, B=B, A=18, D=128)
+        batches.append(pack_records(b["obs"], b["mu"], b["actions"], b["rewards"], b["discounts"],
+                                    entry_size=T + 1))
+    L1, L2 = mk(T=T, B=B, seed=9, optimizer="adam"), mk(T=T, B=B, seed=9, optimizer="adam")
+    for e in batches:
+        s1 = L1.step(e)
+    for e in batches:
+        ent = [bytes(x) for x in e]
+        L2.step_async(ent)
+        del ent  # the call copied them
+    s2 = L2.wait()
+    np.testing.assert_array_equal(L1.get_params(), L2.get_params())
+    assert s1["total_loss"] == s2["total_loss"] and s1["version"] == s2["version"] == 2
+
+
+def test_state_checkpoint_resume_is_bit_exact():
+    """save_state after one step, load it into a fresh learner, step both on the same batch:
+    identical parameters and Adam moments (optimizer state restored, not just weights)."""
+    L1 = mk(T=5, B=16, optimizer="adam", seed=3)
+    L1.synth(seed=8)
+    L1.step_resident()
+    blob = L1.save_state()
+    L2 = mk(T=5, B=16, optimizer="adam", seed=77)
+    L2.synth(seed=8)
+    L2.load_state(blob)
+    np.testing.assert_array_equal(L1.get_params(), L2.get_params())
+    a, b = L1.step_resident(), L2.step_resident()
+    np.testing.assert_array_equal(L1.get_params(), L2.get_params())
+    np.testing.assert_array_equal(L1.tensor("adam_v"), L2.tensor("adam_v"))
+    assert a["version"] == b["version"] == 2
+    from freeimpala_amd._abi import FiError
+    with pytest.raises(FiError):
+        L2.load_state(blob[:-4])
