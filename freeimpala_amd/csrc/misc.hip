@@ -205,18 +205,32 @@ int heads_colsum_partial(const HeadsGrad& g, int splits, float* slab, hipStream_
     return FI_OK;
 }
 
-__global__ void reduce_slabs_kernel(const float* __restrict__ slab, int splits, size_t count,
-                                    float* __restrict__ out) {
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < count;
-         i += (size_t)gridDim.x * blockDim.x) {
-        float s = 0.f;
-        for (int k = 0; k < splits; ++k) s += slab[(size_t)k * count + i];
-        out[i] = s;
+// out[i] = sum_k slab[k][i] over `splits` fp32 partial slabs, in a fixed order (deterministic):
+// a block owns 64 consecutive outputs (one per lane); its 4 waves take the splits k = w mod 4
+// (4 independent accumulators each) and their partials are combined in wave order.
+__global__ __launch_bounds__(256) void reduce_slabs_kernel(const float* __restrict__ slab, int splits,
+                                                           size_t count, float* __restrict__ out) {
+    __shared__ float red[4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const size_t i = (size_t)blockIdx.x * 64 + lane;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    if (i < count) {
+        int k = w;
+        for (; k + 12 < splits; k += 16) {
+            a0 += slab[(size_t)k * count + i];
+            a1 += slab[(size_t)(k + 4) * count + i];
+            a2 += slab[(size_t)(k + 8) * count + i];
+            a3 += slab[(size_t)(k + 12) * count + i];
+        }
+        for (; k < splits; k += 4) a0 += slab[(size_t)k * count + i];
     }
+    red[w][lane] = (a0 + a1) + (a2 + a3);
+    __syncthreads();
+    if (w == 0 && i < count) out[i] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
 
 int reduce_slabs(const float* slab, int splits, size_t count, float* out, hipStream_t s) {
-    hipLaunchKernelGGL(reduce_slabs_kernel, dim3(grid_for(count)), dim3(256), 0, s, slab, splits,
+    hipLaunchKernelGGL(reduce_slabs_kernel, dim3((unsigned)((count + 63) / 64)), dim3(256), 0, s, slab, splits,
                        count, out);
     FI_HIP_CHECK(hipGetLastError());
     return FI_OK;
