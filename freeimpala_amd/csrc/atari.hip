@@ -522,6 +522,138 @@ static int relu_mask_bf16(__bf16* y, const __bf16* m, size_t n, hipStream_t s) {
     return FI_OK;
 }
 
+// ------------------------------------------------------------------ heads backward (VALU)
+// The heads are a 512 x (A+1) layer: K = A+1 = 19 is far too thin for MFMA tiles, so both
+// backward products run on packed fp32 VALU with the weights / accumulators in registers.
+// A wave owns one row at a time (the row's upstream gradient dout[A+1] is wave-uniform:
+// scalar loads), each lane 8 consecutive hidden units.
+//   dgrad: dh[r][j] = (h[r][j] > 0) * sum_o dout[r][o] Wh[j][o]
+//   wgrad: dWh[j][o] = sum_r h[r][j] dout[r][o],  dbh[o] = sum_r dout[r][o]
+template <int O>
+__device__ __forceinline__ void heads_dout_row(const float* __restrict__ dlog, const float* __restrict__ dval,
+                                               int r, int TB, float (&d)[O]) {
+    constexpr int A = O - 1;
+    if (r < TB) {
+#pragma unroll
+        for (int o = 0; o < A; ++o) d[o] = dlog[(size_t)r * A + o];
+    } else {
+#pragma unroll
+        for (int o = 0; o < A; ++o) d[o] = 0.f;
+    }
+    d[A] = dval[r];
+}
+
+template <int O>
+__global__ __launch_bounds__(256, 2) void heads_dgrad_valu(const float* __restrict__ dlog,
+                                                           const float* __restrict__ dval,
+                                                           const float* __restrict__ wh,  // [512][O] fp32
+                                                           const __bf16* __restrict__ h,
+                                                           __bf16* __restrict__ dh, int R, int TB) {
+    const int lane = threadIdx.x & 63, j0 = 8 * lane;
+    float w[8][O];
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj)
+#pragma unroll
+        for (int o = 0; o < O; ++o) w[jj][o] = wh[(size_t)(j0 + jj) * O + o];
+    const int nw = gridDim.x * (blockDim.x >> 6);
+    int r = blockIdx.x * (blockDim.x >> 6) + wave_id();
+    float d[O];
+    if (r < R) heads_dout_row<O>(dlog, dval, r, TB, d);
+    for (; r < R; r += nw) {
+        float dn[O];  // next row's upstream gradient, loaded while this row computes
+        if (r + nw < R) heads_dout_row<O>(dlog, dval, r + nw, TB, dn);
+        float acc[8];
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+            float a = 0.f;
+#pragma unroll
+            for (int o = 0; o < O; ++o) a = fmaf(d[o], w[jj][o], a);
+            acc[jj] = a;
+        }
+        const bf16x8 hv = *(const bf16x8*)(h + (size_t)r * 512 + j0);
+        bf16x8 out;
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) out[jj] = (float)hv[jj] > 0.f ? (__bf16)acc[jj] : (__bf16)0.f;
+        *(bf16x8*)(dh + (size_t)r * 512 + j0) = out;
+#pragma unroll
+        for (int o = 0; o < O; ++o) d[o] = dn[o];
+    }
+}
+
+template <int O>
+__global__ __launch_bounds__(256, 1) void heads_wgrad_valu(const float* __restrict__ dlog,
+                                                           const float* __restrict__ dval,
+                                                           const __bf16* __restrict__ h,
+                                                           float* __restrict__ slab,     // [grid][512][O]
+                                                           float* __restrict__ cs_slab,  // [grid][O]
+                                                           int R, int TB) {
+    __shared__ float red[512 * O];
+    __shared__ float bred[4][O];
+    const int lane = threadIdx.x & 63, j0 = 8 * lane, w = wave_id();
+    float acc[8][O], bs[O];
+#pragma unroll
+    for (int o = 0; o < O; ++o) {
+        bs[o] = 0.f;
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) acc[jj][o] = 0.f;
+    }
+    const int nw = gridDim.x * (blockDim.x >> 6);
+    int r = blockIdx.x * (blockDim.x >> 6) + w;
+    float d[O];
+    if (r < R) heads_dout_row<O>(dlog, dval, r, TB, d);
+    for (; r < R; r += nw) {
+        float dn[O];  // next row's upstream gradient, loaded while this row accumulates
+        if (r + nw < R) heads_dout_row<O>(dlog, dval, r + nw, TB, dn);
+        const bf16x8 hv = *(const bf16x8*)(h + (size_t)r * 512 + j0);
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+            const float x = (float)hv[jj];
+#pragma unroll
+            for (int o = 0; o < O; ++o) acc[jj][o] = fmaf(x, d[o], acc[jj][o]);
+        }
+#pragma unroll
+        for (int o = 0; o < O; ++o) {
+            bs[o] += d[o];
+            d[o] = dn[o];
+        }
+    }
+    // fixed-order combine of the block's 4 waves, then one slab per block
+    for (int i = threadIdx.x; i < 512 * O; i += blockDim.x) red[i] = 0.f;
+    __syncthreads();
+    for (int ww = 0; ww < 4; ++ww) {
+        if (w == ww) {
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj)
+#pragma unroll
+                for (int o = 0; o < O; ++o) red[(j0 + jj) * O + o] += acc[jj][o];
+            if (lane == 0)
+#pragma unroll
+                for (int o = 0; o < O; ++o) bred[ww][o] = bs[o];
+        }
+        __syncthreads();
+    }
+    for (int i = threadIdx.x; i < 512 * O; i += blockDim.x) slab[(size_t)blockIdx.x * 512 * O + i] = red[i];
+    if (threadIdx.x < O)
+        cs_slab[(size_t)blockIdx.x * O + threadIdx.x] =
+            (bred[0][threadIdx.x] + bred[1][threadIdx.x]) + (bred[2][threadIdx.x] + bred[3][threadIdx.x]);
+}
+
+constexpr int kHeadsGrid = 512;
+
+static int heads_wgrad_launch(const float* dlog, const float* dval, const __bf16* h, float* slab, float* cs, int R,
+                              int TB, hipStream_t s) {
+    hipLaunchKernelGGL(heads_wgrad_valu<19>, dim3(kHeadsGrid), dim3(256), 0, s, dlog, dval, h, slab, cs, R, TB);
+    FI_HIP_CHECK(hipGetLastError());
+    return FI_OK;
+}
+
+static int heads_dgrad_launch(const float* dlog, const float* dval, const float* wh, const __bf16* h, __bf16* dh,
+                              int R, int TB, hipStream_t s) {
+    hipLaunchKernelGGL(heads_dgrad_valu<19>, dim3(1024), dim3(256), 0, s, dlog, dval, wh, h, dh, R, TB);
+    FI_HIP_CHECK(hipGetLastError());
+    return FI_OK;
+}
+
 // ------------------------------------------------------------------ weight layouts (bf16)
 struct WeightsBf16 {
     __bf16 *c1T, *c2T, *c3T, *fcT, *hT;  // forward B operands [out][k]
@@ -726,11 +858,18 @@ int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, con
     int rc;
 #define FI_A(tag, x) do { TagScope ts_(tg, tag); rc = (x); if (rc) return rc; } while (0)
     // heads: wgrad [512][O] + bias, dgrad -> dh (masked by h)
-    FI_A("heads_wgrad", (wgrad<128, 32, 4, 1>(RowsBf16{I->h, N, FCO}, dout, slab, cs, N, FCO, O, SPL_H, 1.f, s)));
-    FI_A("reduce_slabs", reduce_slabs(slab, SPL_H, (size_t)FCO * O, grads + o.hw, s));
-    FI_A("reduce_slabs", reduce_slabs(cs, SPL_H, (size_t)O, grads + o.hb, s));
-    FI_A("heads_dgrad", (gemm<128, 128, 2, 2>(dout, RowsBf16{I->wb.hD, FCO, HP}, EpiMaskBf16{I->dh, I->h, FCO}, N, FCO,
-                               HP, s)));
+    if (O == 19) {  // packed-fp32 VALU kernels (A = 18, the configured action set)
+        FI_A("heads_wgrad", heads_wgrad_launch(dlogits, dvalue, I->h, slab, cs, N, I->TB, s));
+        FI_A("reduce_slabs", reduce_slabs(slab, kHeadsGrid, (size_t)FCO * O, grads + o.hw, s));
+        FI_A("reduce_slabs", reduce_slabs(cs, kHeadsGrid, (size_t)O, grads + o.hb, s));
+        FI_A("heads_dgrad", heads_dgrad_launch(dlogits, dvalue, I->params + o.hw, I->h, I->dh, N, I->TB, s));
+    } else {
+        FI_A("heads_wgrad", (wgrad<128, 32, 4, 1>(RowsBf16{I->h, N, FCO}, dout, slab, cs, N, FCO, O, SPL_H, 1.f, s)));
+        FI_A("reduce_slabs", reduce_slabs(slab, SPL_H, (size_t)FCO * O, grads + o.hw, s));
+        FI_A("reduce_slabs", reduce_slabs(cs, SPL_H, (size_t)O, grads + o.hb, s));
+        FI_A("heads_dgrad", (gemm<128, 128, 2, 2>(dout, RowsBf16{I->wb.hD, FCO, HP}, EpiMaskBf16{I->dh, I->h, FCO}, N, FCO,
+                                   HP, s)));
+    }
     // fc: wgrad [3136][512] + bias, dgrad -> da3 (masked by a3)
     // fc (hipBLASLt): wgrad straight into the gradient blob, bias = column sums of dh,
     // dgrad -> da3 unmasked (conv3's backward applies the a3 ReLU mask as it loads da3)

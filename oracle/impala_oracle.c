@@ -442,8 +442,10 @@ int orc_atari_backward_ex(int N, int A, const uint8_t* frames, const float* para
     float* d1 = (float*)malloc((size_t)N * 400 * 32 * sizeof(float));
     if (!x0 || !dh || !d3 || !d2 || !d1) { free(x0); free(dh); free(d3); free(d2); free(d1); return -2; }
     for (size_t i = 0; i < nx; ++i) x0[i] = (float)frames[i];
-    dense_wgrad(N, 512, O, h, dout, emul, grads + off[8], grads + off[9]);
-    dense_dgrad(N, 512, O, dout, params + off[8], h, emul, dh);
+    /* the device runs the heads backward in fp32 (packed VALU, K = A+1 is too thin for MFMA):
+     * no operand rounding there, even in bf16-emulation mode (h is bf16-valued already) */
+    dense_wgrad(N, 512, O, h, dout, 0, grads + off[8], grads + off[9]);
+    dense_dgrad(N, 512, O, dout, params + off[8], h, 0, dh);
     dense_wgrad(N, 3136, 512, a3, dh, emul, grads + off[6], grads + off[7]);
     dense_dgrad(N, 3136, 512, dh, params + off[6], a3, emul, d3);
     conv_wgrad(N, 9, 64, 3, 1, 64, a2, d3, 1.0f, emul, grads + off[4], grads + off[5]);
