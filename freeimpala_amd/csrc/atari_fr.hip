@@ -790,38 +790,48 @@ __global__ __launch_bounds__(512, 2) void conv2_bwd_fr(const __bf16* __restrict_
             }
         }
     } else {
-        // ---------------- data gradient, parity class (wr>>1, wr&1); two row tiles in flight
+        // ---------------- data gradient, parity class (wr>>1, wr&1), transposed on 16x16x32:
+        // D[ci][pixel] = W_cls^T dYcol^T with the class slice of W2 as the register-resident A
+        // operand (32 channels = 2 tiles); 7 pixel tiles of 16 cover the class's 100 pixels
         __bf16* outt = (__bf16*)(smem + c2::RING * c2::SLOT);
-        bf16x8 bw[16];  // W[k = 16ks + 8h + j][ci = col] of class wr
+        bf16x8 bw[2][8];  // lane holds W[ci = 16nt + (lane&15)][k = 32ks + 8g..+8] of class wr
 #pragma unroll
-        for (int ks = 0; ks < 16; ++ks)
-            bw[ks] = *(const bf16x8*)(w2d + ((size_t)(wr * 32 + col)) * 256 + ks * 16 + h * 8);
-        int bd[4];  // dY row of (iyq - ty, ixq - tx) = base - 144*(11 ty + tx)
+        for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-        for (int rt = 0; rt < 4; ++rt) {
-            const int r = min(rt * 32 + col, 99), iyq = r / 10, ixq = r - 10 * iyq;
-            bd[rt] = c2::XB + DP * ((iyq + 1) * 11 + ixq + 1 - 12) + 16 * h;
+            for (int ks = 0; ks < 8; ++ks)
+                bw[nt][ks] = *(const bf16x8*)(w2d + ((size_t)(wr * 32 + 16 * nt + (lane & 15))) * 256 + 32 * ks + 8 * g);
+        int bd[7];  // dY row of (iyq - ty, ixq - tx) = base - 144*(11 ty + tx), channel chunk g
+#pragma unroll
+        for (int pt = 0; pt < 7; ++pt) {
+            const int r = min(pt * 16 + (lane & 15), 99), iyq = r / 10, ixq = r - 10 * iyq;
+            bd[pt] = c2::XB + DP * ((iyq + 1) * 11 + ixq + 1 - 12) + 16 * g;
         }
         c2_frames(ctx, smem, [&](const char* X) {
+            f32x4 acc[7][2];
 #pragma unroll
-            for (int rp = 0; rp < 2; ++rp) {
-                f32x16 acc0 = {}, acc1 = {};
-                const char* base0 = X + bd[2 * rp];
-                const char* base1 = X + bd[2 * rp + 1];
+            for (int pt = 0; pt < 7; ++pt) { acc[pt][0] = f32x4{}; acc[pt][1] = f32x4{}; }
 #pragma unroll
-                for (int ks = 0; ks < 16; ++ks) {
-                    const int tap = ks >> 2, ty = tap >> 1, tx = tap & 1;
-                    const int off = DP * (12 - (11 * ty + tx)) + 32 * (ks & 3);
-                    const bf16x8 a0 = *(const bf16x8*)(base0 + off);
-                    const bf16x8 a1v = *(const bf16x8*)(base1 + off);
-                    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bw[ks], acc0, 0, 0, 0);
-                    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1v, bw[ks], acc1, 0, 0, 0);
+            for (int ks = 0; ks < 8; ++ks) {  // k = 64 tap + co: tap = ks>>1, co half = ks&1
+                const int tap = ks >> 1, ty = tap >> 1, tx = tap & 1;
+                const int off = DP * (12 - (11 * ty + tx)) + 64 * (ks & 1);
+#pragma unroll
+                for (int pt = 0; pt < 7; ++pt) {
+                    const bf16x8 b = *(const bf16x8*)(X + bd[pt] + off);
+                    acc[pt][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[0][ks], b, acc[pt][0], 0, 0, 0);
+                    acc[pt][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[1][ks], b, acc[pt][1], 0, 0, 0);
                 }
+            }
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int ri = rp * 64 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    outt[(wr * 100 + ri) * 32 + col] = (__bf16)acc0[r];
-                    if (ri + 32 < 100) outt[(wr * 100 + ri + 32) * 32 + col] = (__bf16)acc1[r];
+            for (int pt = 0; pt < 7; ++pt) {
+                const int ri = pt * 16 + (lane & 15);
+                if (ri < 100) {
+#pragma unroll
+                    for (int nt = 0; nt < 2; ++nt) {
+                        bf16x4 o;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) o[r] = (__bf16)acc[pt][nt][r];
+                        *(bf16x4*)(outt + (wr * 100 + ri) * 32 + 16 * nt + 4 * g) = o;
+                    }
                 }
             }
         });
