@@ -27,6 +27,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
@@ -65,6 +66,41 @@ static void st_report(const char* name) {
 #define ST() do {} while (0)
 #define ST_FLUSH() do {} while (0)
 static void st_report(const char*) {}
+#endif
+
+#ifdef FI_PHASES  // timing experiment: per-phase clock sums of waves 0 and 4, per workgroup
+__device__ unsigned long long fi_phases[1024 * 16];
+#define PH_DECL unsigned long long ph_[6] = {0, 0, 0, 0, 0, 0}, pt_ = __builtin_amdgcn_s_memtime(); int pn_ = 0;
+#define PH(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); ph_[k] += t_ - pt_; pt_ = t_; } while (0)
+#define PH_ITER() (++pn_)
+#define PH_FLUSH() do { const int w_ = wave_id(); if ((threadIdx.x & 63) == 0 && (w_ == 0 || w_ == 4) && blockIdx.x < 1024) { \
+    for (int k_ = 0; k_ < 6; ++k_) fi_phases[blockIdx.x * 16 + (w_ ? 8 : 0) + k_] = ph_[k_]; \
+    fi_phases[blockIdx.x * 16 + (w_ ? 8 : 0) + 7] = pn_; } } while (0)
+#include <cstdio>
+#include <vector>
+static void ph_report(const char* name, int grid) {
+    static int calls = 0;
+    if (++calls != 4) return;
+    (void)hipDeviceSynchronize();
+    std::vector<unsigned long long> h(1024 * 16);
+    (void)hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(fi_phases), h.size() * 8);
+    for (int r = 0; r < 2; ++r) {
+        double sum[6] = {0}, n = 0;
+        for (int b = 0; b < grid && b < 1024; ++b) {
+            for (int k = 0; k < 6; ++k) sum[k] += (double)h[b * 16 + 8 * r + k];
+            n += (double)h[b * 16 + 8 * r + 7];
+        }
+        std::fprintf(stderr, "[phases %s wave %d] clk/frame:", name, 4 * r);
+        for (int k = 0; k < 6; ++k) std::fprintf(stderr, " %.0f", sum[k] / (n > 0 ? n : 1));
+        std::fprintf(stderr, "\n");
+    }
+}
+#else
+#define PH_DECL
+#define PH(k) do {} while (0)
+#define PH_ITER() do {} while (0)
+#define PH_FLUSH() do {} while (0)
+static void ph_report(const char*, int) {}
 #endif
 
 namespace c1 {
@@ -618,15 +654,40 @@ __device__ __forceinline__ uint32_t dy_piece_off(int P, int npix_side, int pad) 
     return inside ? (uint32_t)(((ry - pad) * npix_side + (rx - pad)) * 128 + 16 * c) : FI_OOB;
 }
 
+// conv2 backward LDS images (bank-conflict-free for every fragment read; MI355X_MICROARCH.md
+// §LDS: a wave's ds_read_b128 is served in 16-lane groups, ds_read_b64_tr_b16 in 32-lane
+// groups, each group conflict-free when its lanes cover 256 distinct bytes mod 256):
+//   X (a1, 20x20x32): parity-class planes, pixel (iy, ix) -> plane 2(iy&1) + (ix&1), position
+//     (iy>>1)*10 + (ix>>1), 64 B per pixel. The wgrad im2col read of 4 consecutive output
+//     pixels then hits 4 consecutive positions (a 256-B run) and every tap is an immediate.
+//   dY (da2, 9x9x64, zero border): 16-B channel chunk c of bordered pixel (Y, X) at unit
+//     s + 128c + Z(c), s = 10Y + X, Z(c) = 8(c&1) + 4((c>>1)&1). Rows are 10 units apart, so
+//     the right border (Y, 10) aliases (Y+1, 0) -- both zero. A class pixel ri of the dgrad
+//     reads s = ri + 11 - 10kty - ktx, i.e. bank unit ri + const, and chunks c, c+1 sit 8
+//     units apart: with lanes 8..15 of each 16-pixel tile swapped by 4 (sig below) the two
+//     16-lane groups of a ds_read_b128 are conflict-free. The wgrad walks the reduction over
+//     s = 11..106 (zero where dY is border), 4 consecutive s x chunk offsets {0, 8, 4, 12}.
+// Both images arrive by LDS-DMA gathers whose per-lane source offsets sit in LDS tables.
 namespace c2 {
-constexpr int XB = 20 * 20 * 64;             // 25,600: a1 tile, linear NHWC
-constexpr int DYB = 18 * 1024;               // 11x11 bordered rows * 144 B = 17,424 -> 18 KiB
-constexpr int SLOT = XB + DYB;               // 44,032
+constexpr int XB = 20 * 20 * 64;             // 25,600: a1 image (class planes)
+constexpr int DYB = 16 * 1024;               // 1,019 used units of 16 B -> 16 KiB
+constexpr int SLOT = XB + DYB;               // 41,984
 constexpr int RING = 3;
-constexpr int NX = XB / 1024, NDY = 18;  // 25 + 18 pieces
-constexpr int OUTT = 4 * 100 * 64;           // dgrad tile [class][100][32 ci] bf16
-constexpr int OUT_CH = XB / 16;              // 1600
+constexpr int NX = XB / 1024, NDY = DYB / 1024;  // 25 + 16 pieces
+static_assert(NX + NDY == 41, "c2_issue assigns 10 pieces to each of waves 0-3 + 1 to wave 0");
+__host__ __device__ constexpr int zc(int c) { return 8 * (c & 1) + 4 * ((c >> 1) & 1); }
 }  // namespace c2
+
+__device__ __forceinline__ uint32_t c2_x_src(int u) {  // X image unit -> a1 byte offset
+    const int P = u / 400, rem = u - 400 * P, pos = rem >> 2, c = rem & 3;
+    const int py = pos / 10, px = pos - 10 * py;
+    return (uint32_t)(((2 * py + (P >> 1)) * 20 + 2 * px + (P & 1)) * 64 + 16 * c);
+}
+__device__ __forceinline__ uint32_t c2_dy_src(int v) {  // dY image unit -> da2 byte offset
+    const int c = v >> 7, k = (v & 127) - c2::zc(c), Y = k / 10, X = k - 10 * Y;
+    const bool inside = k >= 0 && k <= 110 && Y >= 1 && Y <= 9 && X >= 1 && X <= 9;
+    return inside ? (uint32_t)(((Y - 1) * 9 + X - 1) * 128 + 16 * c) : FI_OOB;
+}
 
 // 8 waves, two per SIMD: waves 0-3 compute the weight gradient (wave = kernel row ky),
 // waves 4-7 the data gradient (wave = parity class), sharing one frame pipeline.
@@ -636,90 +697,80 @@ struct C2Ctx {
     int nframes;
 };
 
-// pieces j = w + 8i (< 43) of frame f: X 0..24, dY 25..42 (zero-bordered)
-__device__ __forceinline__ void c2_issue8(const C2Ctx& c, const uint32_t* dyo, int f, uint32_t slot_lds, int w,
-                                          int lane) {
+// pieces j = w + 4i (< 41) of frame f, X 0..24 and dY 25..40, issued by the weight-gradient
+// waves w = 0..3 only (ten each, an eleventh for wave 0): their MFMA work is the shorter one,
+// and the data-gradient waves' 16-byte dX stores would otherwise sit in front of the DMA in
+// their memory queue. All table reads first (one LDS round trip), base + immediate
+// addressing, the X/dY switch a scalar select.
+__device__ __forceinline__ void c2_issue(const C2Ctx& c, const uint32_t* tab, int f, uint32_t slot_lds, int w,
+                                         int lane) {
     const fi_i32x4 xr = make_rsrc(c.a1 + (size_t)f * 12800, 25600);
     const fi_i32x4 dr = make_rsrc(c.da2 + (size_t)f * 5184, 10368);
+    const uint32_t* tb = tab + 64 * w + lane;
+    uint32_t o[11];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
-        const int j = w + 8 * i;
-        if (j < c2::NX) blds16(xr, 16 * lane + 1024 * j, slot_lds + j * 1024);
-        else if (j < c2::NX + c2::NDY)
-            blds16(dr, dyo[64 * (j - c2::NX) + lane], slot_lds + c2::XB + (j - c2::NX) * 1024);
+    for (int i = 0; i < 10; ++i) o[i] = tb[256 * i];
+    if (w == 0) o[10] = tb[256 * 10];
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const int j = w + 4 * i;
+        blds16(j < c2::NX ? xr : dr, o[i], slot_lds + j * 1024);
     }
+    if (w == 0) blds16(dr, o[10], slot_lds + 40 * 1024);
 }
 
 template <class Work>
-__device__ __forceinline__ void c2_frames(const C2Ctx& c, char* smem, Work&& work) {
+__device__ __forceinline__ void c2_frames(const C2Ctx& c, char* smem, int nst, Work&& work) {
     const int lane = threadIdx.x & 63, w = wave_id(), tid = threadIdx.x;
     const uint32_t lds0 = lds_addr(smem);
-    const __bf16* outt = (const __bf16*)(smem + c2::RING * c2::SLOT);
-    // byte offsets of every zero-bordered dY piece (FI_OOB for border / pad slots)
-    uint32_t* dyo = (uint32_t*)(smem + c2::RING * c2::SLOT + c2::OUTT);
-    for (int i = tid; i < c2::NDY * 64; i += 512) dyo[i] = dy_piece_off(i, 9, 1);
+    // per-unit source offsets of both gathers (FI_OOB for border / gap units)
+    uint32_t* tab = (uint32_t*)(smem + c2::RING * c2::SLOT);
+    for (int i = tid; i < c2::SLOT / 16; i += 512) tab[i] = i < c2::XB / 16 ? c2_x_src(i) : c2_dy_src(i - c2::XB / 16);
     __syncthreads();
-    const int npw = (c2::NX + c2::NDY - w + 7) / 8;  // 6 or 5 pieces per wave
-    const int nst = w == 0 ? 4 : 3;                  // copy-out stores issued (lower bound)
+    const int npw = w == 0 ? 11 : (w < 4 ? 10 : 0);  // pieces per wave
     const int nmine = c.nframes > (int)blockIdx.x ? (c.nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
     ST_DECL
     ST();
-    int issued = 0, m0 = 0, m1 = 0, m2 = 0;
-    for (int i = 0; i < 3 && i < nmine; ++i) {
-        c2_issue8(c, dyo, blockIdx.x + i * gridDim.x, lds0 + i * c2::SLOT, w, lane);
+    int issued = 0, m0 = 0, m1 = 0;
+    for (int i = 0; i < 2 && i < nmine; ++i) {
+#ifndef FI_EXP_NODATA
+        if (w < 4) c2_issue(c, tab, blockIdx.x + i * gridDim.x, lds0 + i * c2::SLOT, w, lane);
+#endif
         issued += npw;
-        if (i == 0) m0 = issued; else if (i == 1) m1 = issued; else m2 = issued;
+        if (i == 0) m0 = issued; else m1 = issued;
     }
+    PH_DECL
     for (int it = 0; it < nmine; ++it) {
         const int f = blockIdx.x + it * gridDim.x;
-        const int slot = it % 3;
-        char* X = smem + slot * c2::SLOT;
+        PH(5);
         wait_vmcnt(issued - m0);
-        lds_barrier();  // frame landed
+        PH(0);
+        lds_barrier();  // frame it landed; frame it-1 consumed by every wave
+        PH(1);
         if (it < 5) ST();
-        work(X);
-        if (it < 5) ST();
-        lds_barrier();  // dgrad tile complete
-        if (it < 5) ST();
-        {  // da1 = (X > 0) * dX in NHWC order: chunk P = pixel P/4, channels 8*(P%4)..+8
-            u32x4* dst = (u32x4*)(c.da1 + (size_t)f * 12800);
-#pragma unroll
-            for (int i = 0; i < (c2::OUT_CH + 511) / 512; ++i) {
-                const int P = tid + 512 * i;
-                if (P < c2::OUT_CH) {
-                    const int pix = P >> 2, ch = P & 3;
-                    const int iy = pix / 20, ix = pix - iy * 20;
-                    const int cls = ((iy & 1) << 1) | (ix & 1), ri = (iy >> 1) * 10 + (ix >> 1);
-                    const bf16x8 v = *(const bf16x8*)(outt + (cls * 100 + ri) * 32 + 8 * ch);
-                    const bf16x8 m = *(const bf16x8*)(X + 16 * P);
-                    bf16x8 o;
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) o[j] = (float)m[j] > 0.f ? v[j] : (__bf16)0.f;
-                    FI_ST16(__builtin_bit_cast(u32x4, o), dst + P);
-                }
-            }
-            issued += nst;
-        }
-        lds_barrier();  // slot fully consumed
-        if (it < 5) ST();
-        int m3 = 0;
-        if (it + 3 < nmine) {
-            // the previous frame's copy-out stores drain before the next DMA pieces queue
-            // behind them (measured: slightly faster than letting them overlap)
-#ifndef FI_NO_DRAIN
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        int m2 = 0;
+        if (it + 2 < nmine) {
+#ifndef FI_EXP_NODATA
+            if (w < 4) c2_issue(c, tab, f + 2 * gridDim.x, lds0 + ((it + 2) % 3) * c2::SLOT, w, lane);
 #endif
-            c2_issue8(c, dyo, blockIdx.x + (it + 3) * gridDim.x, lds0 + slot * c2::SLOT, w, lane);
             issued += npw;
-            m3 = issued;
+            m2 = issued;
         }
+        PH(2);
+#ifndef FI_EXP_NOWORK
+        work(smem + (it % 3) * c2::SLOT, f);
+#endif
+        PH(3);
+        PH_ITER();
+        issued += nst;
+        if (it < 5) ST();
         m0 = m1;
         m1 = m2;
-        m2 = m3;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     ST();
     ST_FLUSH();
+    PH_FLUSH();
 }
 
 __global__ __launch_bounds__(512, 2) void conv2_bwd_fr(const __bf16* __restrict__ a1,
@@ -729,46 +780,65 @@ __global__ __launch_bounds__(512, 2) void conv2_bwd_fr(const __bf16* __restrict_
                                                        float* __restrict__ slab,     // [grid][512][64]
                                                        float* __restrict__ cs_slab,  // [grid][64]
                                                        int nframes) {
-    __shared__ __attribute__((aligned(16))) char smem[c2::RING * c2::SLOT + c2::OUTT + c2::NDY * 64 * 4];
+    __shared__ __attribute__((aligned(16))) char smem[c2::RING * c2::SLOT + c2::SLOT / 16 * 4];
     const int lane = threadIdx.x & 63;
     const int w = wave_id(), wr = w & 3;
     const int g = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3, h = lane >> 5, col = lane & 31;
     const C2Ctx ctx{a1, da2, da1, nframes};
 
     if (w < 4) {
-        // ---------------- weight gradient: taps ky = wr, kx = 0..3 (A base + 64 kx), co halves ct
-        int ba[6][2], bb[6][2];
-#pragma unroll
-        for (int ms = 0; ms < 6; ++ms)
-#pragma unroll
-            for (int hh = 0; hh < 2; ++hh) {
-                const int mu = ms * 16 + 8 * (g >> 1) + q + 4 * hh;
-                const int m = min(mu, 80), oy = m / 9, ox = m - 9 * oy;
-                ba[ms][hh] = 64 * ((2 * oy + wr) * 20 + 2 * ox) + 2 * (16 * (g & 1) + 4 * p4);
-                const int mb = min(mu, 89), by = mb / 9, bx = mb - 9 * by;  // m >= 81 -> zero border
-                bb[ms][hh] = c2::XB + DP * ((by + 1) * 11 + bx + 1) + 2 * (16 * (g & 1) + 4 * p4);
-            }
+        // ---------------- weight gradient: taps ky = wr, kx = 0..3, co halves ct. The reduction
+        // runs over dY units s = 11 + mu (output pixel (oy, ox) = divmod(s - 11, 10); ox = 9 and
+        // s >= 100 are zero border in dY, so whatever the A read there returns adds nothing).
+        // A tap kx: class plane 2(wr&1) + (kx&1), position + (kx>>1) -> immediate 6400(kx&1) + 64(kx>>1).
+        // lane bases for mu = 8(g>>1) + q; step ms and half hh add 16ms + 4hh (linear layouts:
+        // every fragment address is one of two base registers plus an immediate)
+        const int mu0 = 8 * (g >> 1) + q, c = 2 * (g & 1) + (p4 >> 1);
+        const int ba0 = 64 * (200 * (wr & 1) + mu0 + 10 * (wr >> 1)) + 2 * (16 * (g & 1) + 4 * p4);
+        const int bb0 = c2::XB + 16 * (11 + mu0 + 128 * c + c2::zc(c)) + 8 * (p4 & 1);
         f32x16 accw[4][2];
 #pragma unroll
         for (int t = 0; t < 4; ++t) { accw[t][0] = f32x16{}; accw[t][1] = f32x16{}; }
         float bsum0 = 0.f, bsum1 = 0.f;
-        c2_frames(ctx, smem, [&](const char* X) {
-#pragma unroll
-            for (int ms = 0; ms < 6; ++ms) {
-                const bf16x8 b0 = tr2(X + bb[ms][0], X + bb[ms][1]);
-                const bf16x8 b1 = tr2(X + bb[ms][0] + 64, X + bb[ms][1] + 64);
-                if (wr == 0) {
-                    float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) { s0 += (float)b0[j]; s1 += (float)b1[j]; }
-                    bsum0 += s0;
-                    bsum1 += s1;
-                }
+        c2_frames(ctx, smem, 0, [&](const char* X, int) {
+            // software pipeline: the 6 fragments of step ms+1 (12 transposed reads) are issued
+            // between the 8 MFMAs of step ms; sched_group_barrier pins that interleave
+            bf16x8 fb[2][6];  // [0] b0, [1] b1, [2..5] A of kx = 0..3
+            const char* XA = X + ba0;
+            const char* XB_ = X + bb0;
+            auto load = [&](int ms, bf16x8* d) {
+                const int ob = 16 * 16 * ms, oa = 64 * 16 * ms;
+                d[0] = tr2(XB_ + ob, XB_ + ob + 64);
+                d[1] = tr2(XB_ + ob + 8192, XB_ + ob + 64 + 8192);  // chunk + 4
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
-                    const bf16x8 afr = tr2(X + ba[ms][0] + 64 * t, X + ba[ms][1] + 64 * t);
-                    accw[t][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, b0, accw[t][0], 0, 0, 0);
-                    accw[t][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, b1, accw[t][1], 0, 0, 0);
+                    const int ao = oa + 6400 * (t & 1) + 64 * (t >> 1);
+                    d[2 + t] = tr2(XA + ao, XA + ao + 256);
+                }
+            };
+            load(0, fb[0]);
+            __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+#pragma unroll
+            for (int ms = 0; ms < 6; ++ms) {
+                const bf16x8* cur = fb[ms & 1];
+                if (ms + 1 < 6) load(ms + 1, fb[(ms + 1) & 1]);
+                float s0 = 0.f, s1 = 0.f;  // bias: column sums of dY (kept by wave 0)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) { s0 += (float)cur[0][j]; s1 += (float)cur[1][j]; }
+                bsum0 += s0;
+                bsum1 += s1;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    accw[t][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[2 + t], cur[0], accw[t][0], 0, 0, 0);
+                    accw[t][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[2 + t], cur[1], accw[t][1], 0, 0, 0);
+                }
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    if (ms + 1 < 6) {
+                        if (k < 4) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                        else __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    }
                 }
             }
         });
@@ -792,46 +862,69 @@ __global__ __launch_bounds__(512, 2) void conv2_bwd_fr(const __bf16* __restrict_
     } else {
         // ---------------- data gradient, parity class (wr>>1, wr&1), transposed on 16x16x32:
         // D[ci][pixel] = W_cls^T dYcol^T with the class slice of W2 as the register-resident A
-        // operand (32 channels = 2 tiles); 7 pixel tiles of 16 cover the class's 100 pixels
-        __bf16* outt = (__bf16*)(smem + c2::RING * c2::SLOT);
-        bf16x8 bw[2][8];  // lane holds W[ci = 16nt + (lane&15)][k = 32ks + 8g..+8] of class wr
+        // operand; 7 pixel tiles of 16 cover the class's 100 pixels. A row i of channel tile nt
+        // is channel 8(i>>2) + 4nt + (i&3), so lane group g ends with channels 8g..8g+7 of its
+        // pixel in acc[pt][0..1]: one 16-byte store of (a1 > 0) * dX per pixel tile.
+        const int ty = wr >> 1, tx = wr & 1;
+        bf16x8 bw[2][8];  // lane holds W[ci = 8(i>>2) + 4nt + (i&3), i = lane&15][k = 32ks + 8g..+8]
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-            for (int ks = 0; ks < 8; ++ks)
-                bw[nt][ks] = *(const bf16x8*)(w2d + ((size_t)(wr * 32 + 16 * nt + (lane & 15))) * 256 + 32 * ks + 8 * g);
-        int bd[7];  // dY row of (iyq - ty, ixq - tx) = base - 144*(11 ty + tx), channel chunk g
-#pragma unroll
-        for (int pt = 0; pt < 7; ++pt) {
-            const int r = min(pt * 16 + (lane & 15), 99), iyq = r / 10, ixq = r - 10 * iyq;
-            bd[pt] = c2::XB + DP * ((iyq + 1) * 11 + ixq + 1 - 12) + 16 * g;
-        }
-        c2_frames(ctx, smem, [&](const char* X) {
-            f32x4 acc[7][2];
-#pragma unroll
-            for (int pt = 0; pt < 7; ++pt) { acc[pt][0] = f32x4{}; acc[pt][1] = f32x4{}; }
-#pragma unroll
-            for (int ks = 0; ks < 8; ++ks) {  // k = 64 tap + co: tap = ks>>1, co half = ks&1
-                const int tap = ks >> 1, ty = tap >> 1, tx = tap & 1;
-                const int off = DP * (12 - (11 * ty + tx)) + 64 * (ks & 1);
-#pragma unroll
-                for (int pt = 0; pt < 7; ++pt) {
-                    const bf16x8 b = *(const bf16x8*)(X + bd[pt] + off);
-                    acc[pt][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[0][ks], b, acc[pt][0], 0, 0, 0);
-                    acc[pt][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[1][ks], b, acc[pt][1], 0, 0, 0);
-                }
+            for (int ks = 0; ks < 8; ++ks) {
+                const int i = lane & 15, ci = 8 * (i >> 2) + 4 * nt + (i & 3);
+                bw[nt][ks] = *(const bf16x8*)(w2d + ((size_t)(wr * 32 + ci)) * 256 + 32 * ks + 8 * g);
             }
+        // lane i of pixel tile pt holds class pixel ri = 16pt + sig(i), sig swapping lanes 8..15 by 4
+        // dY unit of (iyq + 1, ixq + 1) in chunk g: tiles 0..5 are bd0 + 256pt, tile 6 is clamped;
+        // tap (kty, ktx) adds 11 - 10kty - ktx units
+        const int si = (lane & 15) ^ (((lane & 15) >> 1) & 4);
+        const int bd0 = c2::XB + 16 * (si + 128 * g + c2::zc(g));
+        const int bd6 = c2::XB + 16 * (min(96 + si, 99) + 128 * g + c2::zc(g));
+        c2_frames(ctx, smem, 7, [&](const char* X, int f) {
+            // pixel tile outer: each tile's 16 MFMAs (two accumulator chains; 16x16x32 chains
+            // issue back to back) end in its own masked 16-byte store, so the dX stores spread
+            // over the frame instead of queueing as a burst. The next tile's 8 fragments are
+            // read between the current tile's MFMAs (sched_group_barrier pins the interleave).
+            u32x4* dst = (u32x4*)(ctx.da1 + (size_t)f * 12800);
+            bf16x8 fb[2][8];
+            auto load = [&](int pt, bf16x8* d) {  // k = 64 tap + co: tap = ks>>1, co half = ks&1 (chunk + 4)
+                const char* base = X + (pt < 6 ? bd0 + 256 * pt : bd6);
+#pragma unroll
+                for (int ks = 0; ks < 8; ++ks) {
+                    const int tap = ks >> 1, kty = tap >> 1, ktx = tap & 1;
+                    d[ks] = *(const bf16x8*)(base + 16 * (11 - 10 * kty - ktx) + 8192 * (ks & 1));
+                }
+            };
+            load(0, fb[0]);
+            __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
 #pragma unroll
             for (int pt = 0; pt < 7; ++pt) {
-                const int ri = pt * 16 + (lane & 15);
-                if (ri < 100) {
+                const bf16x8* cur = fb[pt & 1];
+                if (pt + 1 < 7) load(pt + 1, fb[(pt + 1) & 1]);
+                f32x4 acc0 = f32x4{}, acc1 = f32x4{};
 #pragma unroll
-                    for (int nt = 0; nt < 2; ++nt) {
-                        bf16x4 o;
+                for (int ks = 0; ks < 8; ++ks) {
+                    acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[0][ks], cur[ks], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[1][ks], cur[ks], acc1, 0, 0, 0);
+                }
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) o[r] = (__bf16)acc[pt][nt][r];
-                        *(bf16x4*)(outt + (wr * 100 + ri) * 32 + 16 * nt + 4 * g) = o;
+                for (int ks = 0; ks < 8; ++ks) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                    if (pt + 1 < 7) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                }
+                // 7 stores per frame (nst above); tile 6 holds 4 pixels
+                const int ri = pt * 16 + si;
+                if (pt < 6 || ri < 100) {
+                    const int iyq = ri / 10, ixq = ri - 10 * iyq;
+                    const int pix = (2 * iyq + ty) * 20 + 2 * ixq + tx;
+                    const s16x8 m = *(const s16x8*)(X + 64 * (100 * wr + ri) + 16 * g);
+                    bf16x8 o;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        o[r] = m[r] > 0 ? (__bf16)acc0[r] : (__bf16)0.f;
+                        o[4 + r] = m[4 + r] > 0 ? (__bf16)acc1[r] : (__bf16)0.f;
                     }
+                    FI_ST16(__builtin_bit_cast(u32x4, o), dst + 4 * pix + g);
                 }
             }
         });
@@ -844,6 +937,7 @@ int conv2_bwd_fr_launch(const __bf16* a1, const __bf16* da2, const __bf16* w2d, 
                        slab, cs_slab, nframes);
     FI_HIP_CHECK(hipGetLastError());
     st_report("conv2_bwd");
+    ph_report("conv2_bwd", grid);
     return FI_OK;
 }
 
@@ -864,7 +958,6 @@ constexpr int OUTT = 81 * 128;               // dgrad tile [81][64] bf16
 constexpr int OUT_CH = 81 * 8;               // 648
 }  // namespace c3
 
-typedef short s16x8 __attribute__((ext_vector_type(8)));
 
 // 8 waves, two per SIMD: waves 0-3 compute the weight gradient, waves 4-7 the data gradient
 // of the same frame (their register sets differ, so each role keeps its own: wgrad 160
@@ -909,7 +1002,9 @@ __device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, Work&& wor
     ST();
     int issued = 0, m0 = 0, m1 = 0, m2 = 0;
     for (int i = 0; i < 3 && i < nmine; ++i) {
+#ifndef FI_EXP_NODATA
         c3_issue8(c, dyo, blockIdx.x + i * gridDim.x, lds0 + i * c3::SLOT, w, lane);
+#endif
         issued += npw;
         if (i == 0) m0 = issued; else if (i == 1) m1 = issued; else m2 = issued;
     }
@@ -930,7 +1025,9 @@ __device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, Work&& wor
             *dyp = v;
         }
         lds_barrier();  // masked dY visible
+#ifndef FI_EXP_NOWORK
         work(X);
+#endif
         if (it < 5) ST();
         lds_barrier();  // dgrad tile complete
         if (it < 5) ST();
@@ -946,7 +1043,9 @@ __device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, Work&& wor
                     bf16x8 o;
 #pragma unroll
                     for (int j = 0; j < 8; ++j) o[j] = (float)m[j] > 0.f ? v[j] : (__bf16)0.f;
+#ifndef FI_EXP_NODATA
                     FI_ST16(__builtin_bit_cast(u32x4, o), dst + P);
+#endif
                 }
             }
             issued += nst;
@@ -960,7 +1059,9 @@ __device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, Work&& wor
 #ifndef FI_NO_DRAIN
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
+#ifndef FI_EXP_NODATA
             c3_issue8(c, dyo, blockIdx.x + (it + 3) * gridDim.x, lds0 + slot * c3::SLOT, w, lane);
+#endif
             issued += npw;
             m3 = issued;
         }
