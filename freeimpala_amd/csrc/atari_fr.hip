@@ -79,8 +79,13 @@ __device__ unsigned long long fi_phases[1024 * 16];
 #include <cstdio>
 #include <vector>
 static void ph_report(const char* name, int grid) {
-    static int calls = 0;
-    if (++calls != 4) return;
+    static const char* names[8];
+    static int calls[8];
+    int k = 0;
+    while (k < 8 && names[k] && names[k] != name) ++k;
+    if (k == 8) return;
+    names[k] = name;
+    if (++calls[k] != 4) return;
     (void)hipDeviceSynchronize();
     std::vector<unsigned long long> h(1024 * 16);
     (void)hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(fi_phases), h.size() * 8);
@@ -628,31 +633,21 @@ int conv3_fwd_fr_launch(const __bf16* a2, const __bf16* w3t, const float* bias, 
 // upstream gradient dY; the kernel writes dX = (X > 0) * dgrad(dY, W) once and keeps
 // dW / db accumulating in registers across its frames (one fp32 partial slab per
 // workgroup, reduced in a fixed order afterwards). Frames stream through a 3-deep LDS ring
-// filled by LDS-DMA (global_load_lds_dwordx4) with counted vmcnt waits.
+// filled by LDS-DMA gathers (buffer_load_dwordx4 ... lds, per-lane source offsets from an
+// LDS table; border units read out of range and land as zeros) with counted vmcnt waits.
 //
-// Layouts are chosen so that every MFMA fragment address is a per-lane base register plus
-// a compile-time immediate (no per-K-step address arithmetic, registers left for the
-// compiler to keep several LDS reads in flight):
-//   X  : linear NHWC, 2*C bytes per pixel.
-//   dY : zero-bordered (OH + 2*pad)^2 pixel rows, pitch 144 B (8 data + 1 pad slot): the
-//        dgrad gather reads row (base - tap) with no bounds checks, and 16 consecutive
-//        rows hit 16 distinct 16-byte slots (9 is odd) -> conflict-free ds_read_b128.
-//        Border and pad slots are DMA'd from a 16-byte zero buffer in global memory.
-// wgrad: A^T = im2col(X) and B = dY are read with ds_read_b64_tr_b16 (transposed MFMA
-//        operands, reduction over the output pixels).
+// Common rules of both kernels:
+//   * LDS images are laid out so that every fragment read is bank-conflict-free
+//     (scripts/lds_conflicts.py models the reads) AND every fragment address is a per-lane
+//     base register plus a compile-time immediate.
+//   * one barrier per frame: past it, every wave is done with the previous frame, whose
+//     slot takes the DMA of frame + 2 at once.
+//   * the weight-gradient waves issue all DMA (the data-gradient waves carry the dX
+//     stores, which are issue-bound per instruction); dX goes straight from registers
+//     to memory, 16 bytes per lane.
+//   * fragment reads of step k+1 are issued between the MFMAs of step k
+//     (sched_group_barrier pins the interleave).
 // =====================================================================================
-constexpr int DP = 144;  // padded dY pitch (bytes)
-
-__device__ __forceinline__ uint32_t dy_piece_off(int P, int npix_side, int pad) {
-    // physical 16-byte piece P of the zero-bordered dY tile -> byte offset in the frame's
-    // dY (FI_OOB for border / pad slots: the buffer range check returns zeros)
-    const int side = npix_side + 2 * pad;
-    const int R = P / 9, c = P - 9 * R;
-    const int ry = R / side, rx = R - side * ry;
-    const bool inside = R < side * side && c < 8 && ry >= pad && rx >= pad && ry < pad + npix_side &&
-                        rx < pad + npix_side;
-    return inside ? (uint32_t)(((ry - pad) * npix_side + (rx - pad)) * 128 + 16 * c) : FI_OOB;
-}
 
 // conv2 backward LDS images (bank-conflict-free for every fragment read; MI355X_MICROARCH.md
 // §LDS: a wave's ds_read_b128 is served in 16-lane groups, ds_read_b64_tr_b16 in 32-lane
@@ -942,136 +937,200 @@ int conv2_bwd_fr_launch(const __bf16* a1, const __bf16* da2, const __bf16* w2d, 
 }
 
 // ------------------------------------------------------------------------------------
-// conv3 backward (3x3 / stride 1, 9x9x64 -> 7x7x64). dgrad on 16x16x32 MFMAs: wave w owns
-// input channels 16w..16w+15 for all 6 row tiles of 16 input pixels (W3 slice of 18
-// K-steps in registers); wgrad on 32x32x16: k-tile kt = w + 4i = (tap 2i + (w>>1),
-// channel half w&1).
+// conv3 backward (3x3 / stride 1, 9x9x64 -> 7x7x64): same structure as conv2's backward.
+// LDS images (bank-conflict-free for every fragment read; checked by scripts/lds_model_c3):
+//   X (a2): chunk planes, unit p + 96c + Z(c) for pixel p = 9y + x, 16-B channel chunk c.
+//   dY (da3) and M (a3, its ReLU mask): bordered 11x11 (2-pixel border), unit
+//     9Y + X + 128c + Z(c) -- rows 9 units apart, so right-border columns alias the next
+//     row's left border (zeros either way). A dX pixel ri then reads dY unit
+//     ri + 20 - 9ky - kx: bank unit ri + const, and with the tile lanes permuted as in
+//     conv2 (sig) both 16-lane groups of a ds_read_b128 are conflict-free.
+//   The weight-gradient reduction walks s = 20..83 (dY zero where it is border), A pixel
+//     s - 20 + 9ky + kx: 4 consecutive s x chunk offsets {0, 8, 4, 12}.
+// a3 arrives through the same gather table as da3, so the wave that DMAs dY piece j also
+// DMAs mask piece j and applies the mask to its own piece before the frame barrier.
+// Waves 0-3: weight gradient (k-tiles kt = wr + 4i = (tap 2i + (wr>>1), channel half wr&1))
+// and all DMA issue; waves 4-7: data gradient, transposed on 16x16x32 (wave = channel half
+// wr&1 x pixel half wr>>1, W3 slice in registers), dX stored from registers.
 // ------------------------------------------------------------------------------------
 namespace c3 {
-constexpr int XB = 11 * 1024;                // 81 px * 128 B = 10,368, padded to 11 KiB
-constexpr int DYB = 18 * 1024;               // 11x11 bordered rows * 144 B = 17,424
-constexpr int MB = 7 * 1024;                 // a3 tile (ReLU mask of dY): 49 px * 128 B = 6,272
-constexpr int SLOT = XB + DYB + MB;          // 36,864
+constexpr int XB = 12 * 1024;                // 768 units (8 chunk planes of 96)
+constexpr int DYB = 16 * 1024;               // 1,009 used units -> 16 KiB
+constexpr int MB = 16 * 1024;                // a3 image, same layout as dY
+constexpr int SLOT = XB + DYB + MB;          // 45,056
 constexpr int RING = 3;
-constexpr int NX = 11, NDY = 18, NM = 7;     // 11 + 18 + 7 pieces
-constexpr int OUTT = 81 * 128;               // dgrad tile [81][64] bf16
-constexpr int OUT_CH = 81 * 8;               // 648
+constexpr int NX = XB / 1024, NDY = DYB / 1024;  // 12 + 16 (+ 16 mask) pieces
+static_assert(NX == 12 && NDY == 16, "c3_issue assigns 3 X + 4 dY + 4 mask pieces per wave");
+__host__ __device__ constexpr int zc(int c) { return 8 * (c & 1) + 4 * ((c >> 1) & 1); }
 }  // namespace c3
 
+__device__ __forceinline__ uint32_t c3_x_src(int u) {  // X image unit -> a2 byte offset
+    const int c = u / 96, k = u - 96 * c - c3::zc(c);
+    return k >= 0 && k <= 80 ? (uint32_t)(k * 128 + 16 * c) : FI_OOB;
+}
+__device__ __forceinline__ uint32_t c3_dy_src(int v) {  // dY / mask image unit -> da3 / a3 byte offset
+    const int c = v >> 7, k = (v & 127) - c3::zc(c), Y = k / 9, X = k - 9 * Y;
+    const bool inside = k >= 0 && k <= 100 && Y >= 2 && Y <= 8 && X >= 2 && X <= 8;
+    return inside ? (uint32_t)(((Y - 2) * 7 + X - 2) * 128 + 16 * c) : FI_OOB;
+}
 
-// 8 waves, two per SIMD: waves 0-3 compute the weight gradient, waves 4-7 the data gradient
-// of the same frame (their register sets differ, so each role keeps its own: wgrad 160
-// accumulators, dgrad the W3 slice), and one role's LDS waits hide behind the other's MFMAs.
 struct C3Ctx {
     const __bf16 *a2, *da3, *a3;
     __bf16* da2;
     int nframes;
 };
 
-// pieces j = w + 8i (< 36) of frame f: X 0..10, dY 11..28 (zero-bordered), a3 mask 29..35
-__device__ __forceinline__ void c3_issue8(const C3Ctx& c, const uint32_t* dyo, int f, uint32_t slot_lds, int w,
-                                          int lane) {
+// wave w < 4 issues X pieces w, w+4, w+8 and dY / mask pieces w, w+4, w+8, w+12 of frame f
+__device__ __forceinline__ void c3_issue(const C3Ctx& c, const uint32_t* tab, int f, uint32_t slot_lds, int w,
+                                         int lane) {
     const fi_i32x4 xr = make_rsrc(c.a2 + (size_t)f * 5184, 10368);
     const fi_i32x4 dr = make_rsrc(c.da3 + (size_t)f * 3136, 6272);
     const fi_i32x4 mr = make_rsrc(c.a3 + (size_t)f * 3136, 6272);
+    const uint32_t* tx = tab + 64 * w + lane;
+    const uint32_t* td = tab + 64 * (c3::NX + w) + lane;
+    uint32_t ox[3], od[4];
 #pragma unroll
-    for (int i = 0; i < 5; ++i) {
-        const int j = w + 8 * i;
-        if (j < c3::NX) blds16(xr, 16 * lane + 1024 * j, slot_lds + j * 1024);
-        else if (j < c3::NX + c3::NDY)
-            blds16(dr, dyo[64 * (j - c3::NX) + lane], slot_lds + c3::XB + (j - c3::NX) * 1024);
-        else if (j < c3::NX + c3::NDY + c3::NM)
-            blds16(mr, 16 * lane + 1024 * (j - c3::NX - c3::NDY), slot_lds + c3::XB + c3::DYB + (j - c3::NX - c3::NDY) * 1024);
+    for (int i = 0; i < 3; ++i) ox[i] = tx[256 * i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) od[i] = td[256 * i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) blds16(xr, ox[i], slot_lds + (w + 4 * i) * 1024);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        blds16(dr, od[i], slot_lds + c3::XB + (w + 4 * i) * 1024);
+        blds16(mr, od[i], slot_lds + c3::XB + c3::DYB + (w + 4 * i) * 1024);
     }
 }
 
-// frame loop shared by both roles: identical barriers, DMA ring, dY mask, masked copy-out
+// one barrier per frame (see c2_frames); the issuing waves mask their own dY pieces first
 template <class Work>
-__device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, Work&& work) {
+__device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, int nst, Work&& work) {
     const int lane = threadIdx.x & 63, w = wave_id(), tid = threadIdx.x;
     const uint32_t lds0 = lds_addr(smem);
-    const __bf16* outt = (const __bf16*)(smem + c3::RING * c3::SLOT);
-    // byte offsets of every zero-bordered dY piece (FI_OOB for border / pad slots)
-    uint32_t* dyo = (uint32_t*)(smem + c3::RING * c3::SLOT + c3::OUTT);
-    for (int i = tid; i < c3::NDY * 64; i += 512) dyo[i] = dy_piece_off(i, 7, 2);
+    uint32_t* tab = (uint32_t*)(smem + c3::RING * c3::SLOT);
+    for (int i = tid; i < (c3::XB + c3::DYB) / 16; i += 512) tab[i] = i < c3::XB / 16 ? c3_x_src(i) : c3_dy_src(i - c3::XB / 16);
     __syncthreads();
-    const int npw = (c3::NX + c3::NDY + c3::NM - w + 7) / 8;  // 5 or 4 pieces per wave
-    const int nst = w <= 2 ? 2 : 1;                           // copy-out stores issued (lower bound)
+    const int npw = w < 4 ? 11 : 0;
     const int nmine = c.nframes > (int)blockIdx.x ? (c.nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
-    ST_DECL
-    ST();
-    int issued = 0, m0 = 0, m1 = 0, m2 = 0;
-    for (int i = 0; i < 3 && i < nmine; ++i) {
-#ifndef FI_EXP_NODATA
-        c3_issue8(c, dyo, blockIdx.x + i * gridDim.x, lds0 + i * c3::SLOT, w, lane);
-#endif
+    int issued = 0, m0 = 0, m1 = 0;
+    for (int i = 0; i < 2 && i < nmine; ++i) {
+        if (w < 4) c3_issue(c, tab, blockIdx.x + i * gridDim.x, lds0 + i * c3::SLOT, w, lane);
         issued += npw;
-        if (i == 0) m0 = issued; else if (i == 1) m1 = issued; else m2 = issued;
+        if (i == 0) m0 = issued; else m1 = issued;
     }
+    PH_DECL
     for (int it = 0; it < nmine; ++it) {
         const int f = blockIdx.x + it * gridDim.x;
-        const int slot = it % 3;
-        char* X = smem + slot * c3::SLOT;
-        wait_vmcnt(issued - m0);
-        lds_barrier();  // frame landed
-        if (it < 5) ST();
-        if (tid < 392) {  // ReLU mask of the upstream gradient: dY *= (a3 > 0)
-            const int p = tid >> 3, ch = tid & 7, py = p / 7, px = p - 7 * py;
-            bf16x8* dyp = (bf16x8*)(X + c3::XB + DP * ((py + 2) * 11 + px + 2) + 16 * ch);
-            const bf16x8 m = *(const bf16x8*)(X + c3::XB + c3::DYB + 128 * p + 16 * ch);
-            bf16x8 v = *dyp;
+        char* X = smem + (it % 3) * c3::SLOT;
+        PH(5);
+        if (w < 4) {
+            wait_vmcnt(issued - m0);
+            // dY *= (a3 > 0) on this wave's own pieces (units 64(w + 4i) + lane)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = (float)m[j] > 0.f ? v[j] : (__bf16)0.f;
-            *dyp = v;
-        }
-        lds_barrier();  // masked dY visible
-#ifndef FI_EXP_NOWORK
-        work(X);
-#endif
-        if (it < 5) ST();
-        lds_barrier();  // dgrad tile complete
-        if (it < 5) ST();
-        {
-            u32x4* dst = (u32x4*)(c.da2 + (size_t)f * 5184);
+            for (int i = 0; i < 4; ++i) {
+                s16x8* dyp = (s16x8*)(X + c3::XB + 16 * (64 * (w + 4 * i) + lane));
+                const s16x8 m = *(const s16x8*)((const char*)dyp + c3::DYB);
+                s16x8 v = *dyp;
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const int P = tid + 512 * i;
-                if (P < c3::OUT_CH) {
-                    const int n = P >> 3, ch = P & 7;  // tile chunks are XOR-swizzled by pixel
-                    const bf16x8 v = *(const bf16x8*)(outt + 64 * n + 8 * (ch ^ (n & 7)));
-                    const bf16x8 m = *(const bf16x8*)(X + 16 * P);
-                    bf16x8 o;
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) o[j] = (float)m[j] > 0.f ? v[j] : (__bf16)0.f;
-#ifndef FI_EXP_NODATA
-                    FI_ST16(__builtin_bit_cast(u32x4, o), dst + P);
-#endif
-                }
+                for (int j = 0; j < 8; ++j) v[j] = m[j] > 0 ? v[j] : (short)0;
+                *dyp = v;
             }
-            issued += nst;
         }
-        lds_barrier();  // slot fully consumed
-        if (it < 5) ST();
-        int m3 = 0;
-        if (it + 3 < nmine) {
-            // the previous frame's copy-out stores drain before the next DMA pieces queue
-            // behind them (measured: slightly faster than letting them overlap)
-#ifndef FI_NO_DRAIN
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-#ifndef FI_EXP_NODATA
-            c3_issue8(c, dyo, blockIdx.x + (it + 3) * gridDim.x, lds0 + slot * c3::SLOT, w, lane);
-#endif
+        PH(0);
+        lds_barrier();  // frame it landed and masked; frame it-1 consumed by every wave
+        PH(1);
+        int m2 = 0;
+        if (it + 2 < nmine) {
+            if (w < 4) c3_issue(c, tab, f + 2 * gridDim.x, lds0 + ((it + 2) % 3) * c3::SLOT, w, lane);
             issued += npw;
-            m3 = issued;
+            m2 = issued;
         }
+        PH(2);
+        work(X, f);
+        issued += nst;
+        PH(3);
+        PH_ITER();
         m0 = m1;
         m1 = m2;
-        m2 = m3;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    ST();
-    ST_FLUSH();
+    PH_FLUSH();
+}
+
+// weight gradient of one wave, taps t = 2i + B (B = wr>>1), i < 5 - B
+template <int B>
+__device__ __forceinline__ void c3_wgrad(const C3Ctx& ctx, char* smem, float* slab, float* cs_slab, int wr) {
+    constexpr int NKT = 5 - B;
+    const int lane = threadIdx.x & 63, g = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3, h = lane >> 5;
+    const int mu0 = 8 * (g >> 1) + q;
+    const int ca = 4 * (wr & 1) + 2 * (g & 1) + (p4 >> 1), cb = 2 * (g & 1) + (p4 >> 1);
+    const int ba0 = 16 * (mu0 + 96 * ca + c3::zc(ca)) + 8 * (p4 & 1);
+    const int bb0 = c3::XB + 16 * (20 + mu0 + 128 * cb + c3::zc(cb)) + 8 * (p4 & 1);
+    f32x16 accw[NKT][2];
+#pragma unroll
+    for (int i = 0; i < NKT; ++i) { accw[i][0] = f32x16{}; accw[i][1] = f32x16{}; }
+    float bsum0 = 0.f, bsum1 = 0.f;
+    c3_frames(ctx, smem, 0, [&](const char* X, int) {
+        const char* XA = X + ba0;
+        const char* XB_ = X + bb0;
+        bf16x8 fb[2][NKT + 2];  // [0] b0, [1] b1 (co halves), [2 + i] A of tap 2i + B
+        auto load = [&](int ms, bf16x8* d) {
+            const int o = 16 * 16 * ms;
+            d[0] = tr2(XB_ + o, XB_ + o + 64);
+            d[1] = tr2(XB_ + o + 8192, XB_ + o + 64 + 8192);  // chunk + 4
+#pragma unroll
+            for (int i = 0; i < NKT; ++i) {
+                const int t = 2 * i + B, ky = t / 3, kx = t - 3 * ky;
+                const int oa = o + 16 * (9 * ky + kx);
+                d[2 + i] = tr2(XA + oa, XA + oa + 64);
+            }
+        };
+        load(0, fb[0]);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 * NKT + 4, 0);
+#pragma unroll
+        for (int ms = 0; ms < 4; ++ms) {
+            const bf16x8* cur = fb[ms & 1];
+            if (ms + 1 < 4) load(ms + 1, fb[(ms + 1) & 1]);
+            float s0 = 0.f, s1 = 0.f;  // bias: column sums of dY (kept by wave 0)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { s0 += (float)cur[0][j]; s1 += (float)cur[1][j]; }
+            bsum0 += s0;
+            bsum1 += s1;
+#pragma unroll
+            for (int i = 0; i < NKT; ++i) {
+                accw[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[2 + i], cur[0], accw[i][0], 0, 0, 0);
+                accw[i][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[2 + i], cur[1], accw[i][1], 0, 0, 0);
+            }
+            // 2NKT MFMAs, 2NKT + 4 reads of the next step: pairs of reads between MFMAs
+#pragma unroll
+            for (int k = 0; k < 2 * NKT; ++k) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                if (ms + 1 < 4) {
+                    if (k < NKT + 2) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                    else __builtin_amdgcn_sched_group_barrier(0x100, 0, 0);
+                }
+            }
+        }
+    });
+    float* out = slab + (size_t)blockIdx.x * 576 * 64;
+#pragma unroll
+    for (int i = 0; i < NKT; ++i) {
+        const int kt = wr + 4 * i;
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int k = 32 * kt + (r & 3) + 8 * (r >> 2) + 4 * h;
+                out[k * 64 + 32 * ct + (lane & 31)] = accw[i][ct][r];
+            }
+    }
+    if (wr == 0) {  // lanes l and l+32 hold the same co, other m half
+        const float o0 = __shfl_xor(bsum0, 32, 64), o1 = __shfl_xor(bsum1, 32, 64);
+        if (lane < 32) {
+            cs_slab[(size_t)blockIdx.x * 64 + lane] = bsum0 + o0;
+            cs_slab[(size_t)blockIdx.x * 64 + 32 + lane] = bsum1 + o1;
+        }
+    }
 }
 
 __global__ __launch_bounds__(512, 2) void conv3_bwd_fr(const __bf16* __restrict__ a2,
@@ -1082,127 +1141,78 @@ __global__ __launch_bounds__(512, 2) void conv3_bwd_fr(const __bf16* __restrict_
                                                        float* __restrict__ slab,     // [grid][576][64]
                                                        float* __restrict__ cs_slab,  // [grid][64]
                                                        int nframes) {
-    __shared__ __attribute__((aligned(16))) char smem[c3::RING * c3::SLOT + c3::OUTT + c3::NDY * 64 * 4];
+    __shared__ __attribute__((aligned(16))) char smem[c3::RING * c3::SLOT + (c3::XB + c3::DYB) / 16 * 4];
     const int lane = threadIdx.x & 63;
     const int w = wave_id(), wr = w & 3;
-    const int g = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3, h = lane >> 5;
+    const int g = lane >> 4;
     const C3Ctx ctx{a2, da3, a3, da2, nframes};
 
     if (w < 4) {
-        // ---------------- weight gradient: k-tiles kt = wr + 4i = (tap 2i + (wr>>1), channel half wr&1)
-        int toff[5];
-#pragma unroll
-        for (int i = 0; i < 5; ++i) {
-            const int t = min(2 * i + (wr >> 1), 8), ky = t / 3, kx = t - 3 * ky;
-            toff[i] = __builtin_amdgcn_readfirstlane(128 * (9 * ky + kx));
-        }
-        const int nkt = (18 - wr + 3) / 4;  // 5,5,4,4
-        int ba[4][2], bb[4][2];
-#pragma unroll
-        for (int ms = 0; ms < 4; ++ms)
-#pragma unroll
-            for (int hh = 0; hh < 2; ++hh) {
-                const int mu = ms * 16 + 8 * (g >> 1) + q + 4 * hh;
-                const int m = min(mu, 48), oy = m / 7, ox = m - 7 * oy;
-                ba[ms][hh] = 128 * (oy * 9 + ox) + 2 * (32 * (wr & 1) + 16 * (g & 1) + 4 * p4);
-                const int mb = min(mu, 55), by = mb / 7, bx = mb - 7 * by;  // m >= 49 -> zero border
-                bb[ms][hh] = c3::XB + DP * ((by + 2) * 11 + bx + 2) + 2 * (16 * (g & 1) + 4 * p4);
-            }
-        f32x16 accw[5][2];
-#pragma unroll
-        for (int i = 0; i < 5; ++i) { accw[i][0] = f32x16{}; accw[i][1] = f32x16{}; }
-        float bsum0 = 0.f, bsum1 = 0.f;
-        c3_frames(ctx, smem, [&](const char* X) {
-#pragma unroll
-            for (int ms = 0; ms < 4; ++ms) {
-                const bf16x8 b0 = tr2(X + bb[ms][0], X + bb[ms][1]);
-                const bf16x8 b1 = tr2(X + bb[ms][0] + 64, X + bb[ms][1] + 64);
-                if (wr == 0) {
-                    float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) { s0 += (float)b0[j]; s1 += (float)b1[j]; }
-                    bsum0 += s0;
-                    bsum1 += s1;
-                }
-#pragma unroll
-                for (int i = 0; i < 5; ++i) {
-                    if (i < nkt) {
-                        const bf16x8 afr = tr2(X + ba[ms][0] + toff[i], X + ba[ms][1] + toff[i]);
-                        accw[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, b0, accw[i][0], 0, 0, 0);
-                        accw[i][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr, b1, accw[i][1], 0, 0, 0);
-                    }
-                }
-            }
-        });
-        float* out = slab + (size_t)blockIdx.x * 576 * 64;
-#pragma unroll
-        for (int i = 0; i < 5; ++i) {
-            if (i < nkt) {
-                const int kt = wr + 4 * i;
-#pragma unroll
-                for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int k = 32 * kt + (r & 3) + 8 * (r >> 2) + 4 * h;
-                        out[k * 64 + 32 * ct + (lane & 31)] = accw[i][ct][r];
-                    }
-            }
-        }
-        if (wr == 0) {
-            const float o0 = __shfl_xor(bsum0, 32, 64), o1 = __shfl_xor(bsum1, 32, 64);
-            if (lane < 32) {
-                cs_slab[(size_t)blockIdx.x * 64 + lane] = bsum0 + o0;
-                cs_slab[(size_t)blockIdx.x * 64 + 32 + lane] = bsum1 + o1;
-            }
-        }
+        if (wr >> 1) c3_wgrad<1>(ctx, smem, slab, cs_slab, wr);
+        else c3_wgrad<0>(ctx, smem, slab, cs_slab, wr);
     } else {
-        // ---------------- data gradient (16x16x32), transposed: D[ci][pixel] = W^T dYcol^T with the
-        // W slice as the register-resident A operand. Wave wr: channel tiles 2(wr&1), 2(wr&1)+1
-        // (32 channels), pixel tiles 3(wr>>1)..+2 -- each dY fragment read feeds two MFMAs, and a
-        // lane ends with 4 consecutive channels of one pixel (one 8-byte store).
-        __bf16* outt = (__bf16*)(smem + c3::RING * c3::SLOT);
+        // data gradient: channel half chh = wr&1 (tiles ct = 0, 1 of 16 channels; row i of tile
+        // ct is channel 32chh + 8(i>>2) + 4ct + (i&3), so lane group g ends with channels
+        // 32chh + 8g..+8 of its pixel), pixel tiles 3ph..3ph+2 (ph = wr>>1), lane i of tile pt
+        // on pixel 16pt + sig(i)
         const int chh = wr & 1, ph = wr >> 1;
-        s16x8 bw[2][18];  // lane holds W[k = 32ks + 8g + j][ci = 32chh + 16ct + (lane&15)]
+        s16x8 bw[2][18];  // lane holds W[ci(ct, lane&15)][k = 32ks + 8g..+8]
 #pragma unroll
         for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
-            for (int ks = 0; ks < 18; ++ks)
-                bw[ct][ks] = *(const s16x8*)(w3d + (size_t)(32 * chh + 16 * ct + (lane & 15)) * 576 + 32 * ks + 8 * g);
-        int bd[3];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const int pix = min((3 * ph + i) * 16 + (lane & 15), 80), iy = pix / 9, ix = pix - 9 * iy;
-            bd[i] = c3::XB + DP * ((iy + 2) * 11 + ix + 2 - 24) + 16 * g;
-        }
-        c3_frames(ctx, smem, [&](const char* X) {
+            for (int ks = 0; ks < 18; ++ks) {
+                const int i = lane & 15, ci = 32 * chh + 8 * (i >> 2) + 4 * ct + (i & 3);
+                bw[ct][ks] = *(const s16x8*)(w3d + (size_t)ci * 576 + 32 * ks + 8 * g);
+            }
+        const int si = (lane & 15) ^ (((lane & 15) >> 1) & 4);
+        const int cg = g;  // dY chunk of k-step ks: g + 4(ks&1)
+        const int bdA = c3::XB + 16 * (48 * ph + si + 128 * cg + c3::zc(cg));
+        const int bdC = c3::XB + 16 * (min(48 * ph + 32 + si, 80) + 128 * cg + c3::zc(cg));
+        c3_frames(ctx, smem, 3, [&](const char* X, int f) {
             f32x4 acc[3][2];
 #pragma unroll
-            for (int i = 0; i < 3; ++i) { acc[i][0] = f32x4{}; acc[i][1] = f32x4{}; }
+            for (int ti = 0; ti < 3; ++ti) { acc[ti][0] = f32x4{}; acc[ti][1] = f32x4{}; }
+            bf16x8 fb[2][3];
+            auto load = [&](int ks, bf16x8* d) {  // k = 64 tap + co: tap = ks>>1, co half = ks&1 (chunk + 4)
+                const int tap = ks >> 1, ky = tap / 3, kx = tap - 3 * ky;
+                const int off = 16 * (20 - 9 * ky - kx) + 8192 * (ks & 1);
+                d[0] = *(const bf16x8*)(X + bdA + off);
+                d[1] = *(const bf16x8*)(X + bdA + 256 + off);
+                d[2] = *(const bf16x8*)(X + bdC + off);
+            };
+            load(0, fb[0]);
+            __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
 #pragma unroll
             for (int ks = 0; ks < 18; ++ks) {
-                const int tap = ks >> 1, ky = tap / 3, kx = tap - 3 * ky;
-                const int off = DP * (24 - (11 * ky + kx)) + 64 * (ks & 1);
+                const bf16x8* cur = fb[ks & 1];
+                if (ks + 1 < 18) load(ks + 1, fb[(ks + 1) & 1]);
 #pragma unroll
-                for (int i = 0; i < 3; ++i) {
-                    const bf16x8 b = __builtin_bit_cast(bf16x8, *(const s16x8*)(X + bd[i] + off));
-                    acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bw[0][ks]), b,
-                                                                       acc[i][0], 0, 0, 0);
-                    acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bw[1][ks]), b,
-                                                                       acc[i][1], 0, 0, 0);
+                for (int ti = 0; ti < 3; ++ti) {
+                    acc[ti][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bw[0][ks]), cur[ti],
+                                                                        acc[ti][0], 0, 0, 0);
+                    acc[ti][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bw[1][ks]), cur[ti],
+                                                                        acc[ti][1], 0, 0, 0);
+                }
+#pragma unroll
+                for (int ti = 0; ti < 3; ++ti) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                    if (ks + 1 < 18) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                 }
             }
+            u32x4* dst = (u32x4*)(ctx.da2 + (size_t)f * 5184);
+            const int c = 4 * chh + g;
 #pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                const int pix = (3 * ph + i) * 16 + (lane & 15);
-                if (pix < 81) {
+            for (int ti = 0; ti < 3; ++ti) {  // 3 stores per frame (nst above)
+                const int ri = (3 * ph + ti) * 16 + si;
+                if (ri < 81) {
+                    const s16x8 m = *(const s16x8*)(X + 16 * (ri + 96 * c + c3::zc(c)));
+                    bf16x8 o;
 #pragma unroll
-                    for (int ct = 0; ct < 2; ++ct) {
-                        bf16x4 o;
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) o[r] = (__bf16)acc[i][ct][r];
-                        const int chunk = (4 * chh + 2 * ct + (g >> 1)) ^ (pix & 7);
-                        *(bf16x4*)((char*)outt + 128 * pix + 16 * chunk + 8 * (g & 1)) = o;
+                    for (int r = 0; r < 4; ++r) {
+                        o[r] = m[r] > 0 ? (__bf16)acc[ti][0][r] : (__bf16)0.f;
+                        o[4 + r] = m[4 + r] > 0 ? (__bf16)acc[ti][1][r] : (__bf16)0.f;
                     }
+                    FI_ST16(__builtin_bit_cast(u32x4, o), dst + 8 * ri + c);
                 }
             }
         });
@@ -1215,6 +1225,7 @@ int conv3_bwd_fr_launch(const __bf16* a2, const __bf16* da3, const __bf16* a3, c
                        slab, cs_slab, nframes);
     FI_HIP_CHECK(hipGetLastError());
     st_report("conv3_bwd");
+    ph_report("conv3_bwd", grid);
     return FI_OK;
 }
 
