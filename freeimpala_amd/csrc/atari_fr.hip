@@ -110,11 +110,9 @@ static void ph_report(const char*, int) {}
 
 namespace c1 {
 constexpr int FRAME_LOADS = 84 * 84 * 4 / 16;       // 1764 16-byte loads per frame
-constexpr int PER_T = (FRAME_LOADS + 255) / 256;    // 7
 constexpr int PLANE = 84 * 21 * 16 + 64;            // bytes (+64: plane 1 shifted 4 slots)
 constexpr int IMG = 2 * PLANE;                      // 56,576 B
 constexpr int OUT = 400 * 32 * 2;                   // 25,600 B output / dY tile
-constexpr int OUT_CH = OUT / 16;                    // 1600 16-byte chunks
 }  // namespace c1
 
 __device__ __forceinline__ void u8x16_to_bf16(u32x4 v, bf16x8& lo, bf16x8& hi) {
@@ -122,28 +120,6 @@ __device__ __forceinline__ void u8x16_to_bf16(u32x4 v, bf16x8& lo, bf16x8& hi) {
     for (int j = 0; j < 8; ++j) {
         lo[j] = (__bf16)(float)((v[j >> 2] >> (8 * (j & 3))) & 0xffu);
         hi[j] = (__bf16)(float)((v[2 + (j >> 2)] >> (8 * (j & 3))) & 0xffu);
-    }
-}
-
-__device__ __forceinline__ void c1_fetch_frame(const uint8_t* fr, u32x4 (&r)[c1::PER_T]) {
-    const u32x4* src = (const u32x4*)fr;
-#pragma unroll
-    for (int i = 0; i < c1::PER_T; ++i) {
-        const int u = threadIdx.x + 256 * i;
-        r[i] = u < c1::FRAME_LOADS ? __builtin_nontemporal_load(src + u) : u32x4{0, 0, 0, 0};
-    }
-}
-
-__device__ __forceinline__ void c1_store_image(char* img, const u32x4 (&r)[c1::PER_T]) {
-#pragma unroll
-    for (int i = 0; i < c1::PER_T; ++i) {
-        const int u = threadIdx.x + 256 * i;
-        if (u < c1::FRAME_LOADS) {
-            bf16x8 lo, hi;
-            u8x16_to_bf16(r[i], lo, hi);
-            *(bf16x8*)(img + 16 * u) = lo;
-            *(bf16x8*)(img + c1::PLANE + 16 * u) = hi;
-        }
     }
 }
 
@@ -167,36 +143,37 @@ __device__ __forceinline__ int c1_issue_raw(const uint8_t* fr, uint32_t slot_lds
     return w < 4 ? 4 : 3;
 }
 
-// 512 threads = two waves per SIMD: one wave's LDS / DMA waits hide behind the other's MFMAs.
-// Wave w computes all 32 output channels of the pixel tiles w, w+8, w+16 (, w+24).
+// 512 threads = two waves per SIMD. Wave w computes all 32 output channels of the pixel
+// tiles w, w+8, w+16 (and 24 for wave 0): 16x16x32 MFMAs with the weights as the A operand,
+// D[channel][pixel]; A row i of channel tile nt is channel 8(i>>2) + 4nt + (i&3), so lane
+// group g ends with channels 8g..8g+7 of its pixel and stores them straight to a1 (16 B).
+// Lane i of a tile holds pixel 16t + sig(i) (lanes 8..15 swapped by 4): with the image's
+// plane offset of 8 units (mod 16) both 16-lane groups of every B read are conflict-free.
+// The next tile's 8 B fragments are read between the current tile's MFMAs.
+struct f32x4x2 {
+    f32x4 a, b;
+};
+
 __global__ __launch_bounds__(512, 2) void conv1_fwd_fr(const uint8_t* __restrict__ frames,
                                                        const __bf16* __restrict__ w1t,  // [32][256]
                                                        const float* __restrict__ bias,
                                                        __bf16* __restrict__ a1, int nframes) {
-    __shared__ __attribute__((aligned(16))) char smem[2 * c1::RAW + c1::IMG + c1::OUT];
+    __shared__ __attribute__((aligned(16))) char smem[2 * c1::RAW + c1::IMG];
     char* img = smem + 2 * c1::RAW;
-    __bf16* out = (__bf16*)(smem + 2 * c1::RAW + c1::IMG);
     const int lane = threadIdx.x & 63, w = wave_id();
     const uint32_t lds0 = lds_addr(smem);
-    // 16x16x32 MFMAs with the weights as the A operand: D[channel][pixel], so a lane ends up
-    // with 4 consecutive channels of one pixel (one 8-byte LDS store). K-step ks = kernel row
-    // ky (32 k = 8 taps x 4 channels); W fragments of both channel halves stay in registers:
-    // lane holds W[c = 16nt + (lane&15)][k = 32ks + 8g..+8]
-    const int g = lane >> 4, c16 = lane & 15;
-    bf16x8 bw[2][8];
+    const int g = lane >> 4, c16 = lane & 15, si = c16 ^ ((c16 >> 1) & 4);
+    bf16x8 bw[2][8];  // lane holds W[8(i>>2) + 4nt + (i&3), i = lane&15][k = 32ks + 8g..+8]
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
         for (int ks = 0; ks < 8; ++ks)
-            bw[nt][ks] = *(const bf16x8*)(w1t + (16 * nt + c16) * 256 + 32 * ks + 8 * g);
-    float bch[2][4];  // bias of the lane's output channels 16nt + 4g + r
+            bw[nt][ks] = *(const bf16x8*)(w1t + (8 * (c16 >> 2) + 4 * nt + (c16 & 3)) * 256 + 32 * ks + 8 * g);
+    float bch[8];  // bias of the lane's output channels 8g + j
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) bch[nt][r] = bias[16 * nt + 4 * g + r];
+    for (int j = 0; j < 8; ++j) bch[j] = bias[8 * g + j];
     const float inv255 = 1.0f / 255.0f;
-    constexpr int ST_W = c1::OUT_CH / 512;  // 3 full store rounds (+1 for wave 0)
-    const int stores = ST_W + (w < (c1::OUT_CH - 512 * ST_W) / 64 ? 1 : 0);
+    const int nst = w == 0 ? 4 : 3;  // a1 stores per frame (one per tile)
 
     const int nmine = nframes > (int)blockIdx.x ? (nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
     ST_DECL
@@ -206,11 +183,15 @@ __global__ __launch_bounds__(512, 2) void conv1_fwd_fr(const uint8_t* __restrict
     m0 = issued;
     if (nmine > 1) issued += c1_issue_raw(frames + (size_t)(blockIdx.x + gridDim.x) * 28224, lds0 + c1::RAW, w, lane);
     m1 = issued;
+    PH_DECL
     for (int it = 0; it < nmine; ++it) {
         const int f = blockIdx.x + it * gridDim.x;
         const char* raw = smem + (it & 1) * c1::RAW;
+        PH(5);
         wait_vmcnt(issued - m0);
-        lds_barrier();  // raw frame landed; previous out tile drained, image free
+        PH(0);
+        lds_barrier();  // raw frame landed; every wave done with the previous image
+        PH(1);
         if (it < 6) ST();
 #pragma unroll
         for (int i = 0; i < (c1::FRAME_LOADS + 511) / 512; ++i) {
@@ -222,52 +203,71 @@ __global__ __launch_bounds__(512, 2) void conv1_fwd_fr(const uint8_t* __restrict
                 *(bf16x8*)(img + c1::PLANE + 16 * u) = hi;
             }
         }
+        PH(2);
         lds_barrier();  // image ready; raw slot free
+        PH(1);
         if (it < 6) ST();
         int m2 = issued;
         if (it + 2 < nmine) {
             issued += c1_issue_raw(frames + (size_t)(f + 2 * gridDim.x) * 28224, lds0 + (it & 1) * c1::RAW, w, lane);
             m2 = issued;
         }
-        // 25 tiles of 16 output pixels; this wave: tiles w, w+8, ... (both channel halves)
-        for (int t = w; t < 25; t += 8) {
-            const int q = t * 16 + c16;
-            const int oy = q / 20, ox = q - 20 * oy;
-            // pixel pair (2ox + g) of input row 4oy + ky: plane g&1, slot (4oy+ky)*21 + ox + g/2
+        PH(4);
+        u32x4* dst = (u32x4*)(a1 + (size_t)f * 12800);
+        // B fragments of tile t: pixel pair (4ox + 2g..+1) of input row 4oy + ks -> plane g&1,
+        // unit (4oy + ks) * 21 + ox + (g>>1)
+        auto load = [&](int t, bf16x8* d) {
+            const int q = t * 16 + si, oy = q / 20, ox = q - 20 * oy;
             const char* ab = img + (g & 1) * c1::PLANE + 16 * (oy * 84 + ox + (g >> 1));
-            bf16x8 fa[8];
 #pragma unroll
-            for (int ks = 0; ks < 8; ++ks) fa[ks] = *(const bf16x8*)(ab + 16 * 21 * ks);
-            f32x4 d0 = {}, d1 = {};
+            for (int ks = 0; ks < 8; ++ks) d[ks] = *(const bf16x8*)(ab + 16 * 21 * ks);
+        };
+        auto tile = [&](const bf16x8* cur) {
+            f32x4x2 d = {f32x4{}, f32x4{}};
 #pragma unroll
             for (int ks = 0; ks < 8; ++ks) {
-                d0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[0][ks], fa[ks], d0, 0, 0, 0);
-                d1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[1][ks], fa[ks], d1, 0, 0, 0);
+                d.a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[0][ks], cur[ks], d.a, 0, 0, 0);
+                d.b = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[1][ks], cur[ks], d.b, 0, 0, 0);
             }
-            bf16x4 o0, o1;
+            return d;
+        };
+        auto store = [&](int t, const f32x4x2& d) {
+            const int q = t * 16 + si;
+            bf16x8 o;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                o0[r] = (__bf16)fmaxf(d0[r] * inv255 + bch[0][r], 0.f);
-                o1[r] = (__bf16)fmaxf(d1[r] * inv255 + bch[1][r], 0.f);
+                o[r] = (__bf16)fmaxf(d.a[r] * inv255 + bch[r], 0.f);
+                o[4 + r] = (__bf16)fmaxf(d.b[r] * inv255 + bch[4 + r], 0.f);
             }
-            *(bf16x4*)(out + q * 32 + 4 * g) = o0;
-            *(bf16x4*)(out + q * 32 + 16 + 4 * g) = o1;
-        }
-        lds_barrier();  // out tile complete
-        if (it < 6) ST();
-        u32x4* dst = (u32x4*)(a1 + (size_t)f * 12800);
+            FI_ST16(__builtin_bit_cast(u32x4, o), dst + 4 * q + g);
+        };
+        bf16x8 fb[2][8];
+        load(w, fb[0]);
+        __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
 #pragma unroll
-        for (int i = 0; i < (c1::OUT_CH + 511) / 512; ++i) {
-            const int c = threadIdx.x + 512 * i;
-            if (c < c1::OUT_CH) FI_ST16(((const u32x4*)out)[c], dst + c);
+        for (int tt = 0; tt < 3; ++tt) {
+            const int t = w + 8 * tt;
+            if (tt < 2) load(t + 8, fb[(tt + 1) & 1]);
+            else if (w == 0) load(24, fb[1]);  // wave 0 also takes tile 24
+            const f32x4x2 d = tile(fb[tt & 1]);
+#pragma unroll
+            for (int ks = 0; ks < 8; ++ks) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            }
+            store(t, d);
         }
-        issued += stores;
+        if (w == 0) store(24, tile(fb[1]));
+        issued += nst;
+        PH(3);
+        PH_ITER();
         m0 = m1;
         m1 = m2;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     ST();
     ST_FLUSH();
+    PH_FLUSH();
 }
 
 // ---------------------------------------------------------------------------------
@@ -283,36 +283,45 @@ __device__ __forceinline__ bf16x8 tr2(const char* p0, const char* p1) {
     return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-// 8 waves, wave w = k-tile w (kernel row ky = w: 8 taps x 4 channels = 32 k) for all 32
-// output channels. Per frame: the raw u8 frame (1 slot, prefetched one frame ahead) and the
-// da1 tile (2-slot ring, two frames ahead) arrive by LDS-DMA; the frame is converted once
-// into the bf16 pair-plane image; both MFMA operands come from transposed LDS reads.
+// 8 waves: wave w accumulates k-tiles 4kg..4kg+3 (kg = w&1; k-tile = kernel row ky: 8 taps x
+// 4 channels = 32 k) over the m-steps ms = mg, mg+4, ... (mg = w>>1) of every frame, so each
+// da1 fragment read feeds four MFMAs (LDS reads per MFMA: 1.25 KB instead of 2). The four
+// m-groups' partial sums are reduced in LDS in a fixed order at the end. Per frame: the raw
+// u8 frame (1 slot, issued as soon as the previous one is converted) and the da1 tile
+// (3-slot ring, two frames ahead) arrive by LDS-DMA; the frame is converted once into the
+// bf16 pair-plane image; both MFMA operands come from transposed LDS reads, the next
+// m-step's issued between the current one's MFMAs. Two barriers per frame: past the first,
+// every wave is done with the previous frame (image and its da1 slot free); past the second,
+// the image is complete (raw slot free).
 __global__ __launch_bounds__(512, 2) void conv1_wgrad_fr(const uint8_t* __restrict__ frames,
                                                          const __bf16* __restrict__ da1,
                                                          float* __restrict__ slab,
                                                          float* __restrict__ cs_slab, int nframes) {
-    __shared__ __attribute__((aligned(16))) char smem[c1::RAW + 2 * c1::OUT + c1::IMG];
+    __shared__ __attribute__((aligned(16))) char smem[c1::RAW + 3 * c1::OUT + c1::IMG];
     char* raw = smem;
-    char* img = smem + c1::RAW + 2 * c1::OUT;
+    char* img = smem + c1::RAW + 3 * c1::OUT;
     const uint32_t lds0 = lds_addr(smem);
     const int lane = threadIdx.x & 63, w = wave_id(), tid = threadIdx.x;
     const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-    // lane's tr column: k = 32w + 16(g&1) + 4p = tap (ky = w, kx = 4(g&1) + p) x 4 channels
-    const int toff = w * 84 + 4 * (g & 1) + p;  // pixel offset of the tap relative to (4oy, 4ox)
-    int wao[25][2];  // image offset of the A^T (im2col) transposed read, per m-step / half
+    const int kg = w & 1, mg = w >> 1;
+    // lane's tr column: k = 32ky + 16(g&1) + 4p = tap (ky, kx = 4(g&1) + p) x 4 channels;
+    // ky = 4kg + kt, the kt step is +21 image units (+336 B)
+    const int toff = 4 * kg * 84 + 4 * (g & 1) + p;  // pixel offset of the tap relative to (4oy, 4ox)
+    int wao[7][2];  // image offset of the A^T (im2col) transposed read, per own m-step / half
 #pragma unroll
-    for (int ms = 0; ms < 25; ++ms)
+    for (int j = 0; j < 7; ++j)
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
+            const int ms = min(mg + 4 * j, 24);
             const int m = ms * 16 + 8 * (g >> 1) + q + 4 * hh;
             const int oy = m / 20, ox = m - oy * 20;
             const int P = oy * 4 * 84 + ox * 4 + toff;
             const int y = P / 84, x = P - y * 84;
-            wao[ms][hh] = ((x >> 1) & 1) * c1::PLANE + 16 * (y * 21 + (x >> 2)) + 8 * (x & 1);
+            wao[j][hh] = ((x >> 1) & 1) * c1::PLANE + 16 * (y * 21 + (x >> 2)) + 8 * (x & 1);
         }
     // da1 tile [m][32 co]: B read of rows m = 16ms + 8(g>>1) + q + 4hh -> base_hh + 1024 ms
-    const int wb0 = (8 * (g >> 1) + q) * 64 + (16 * (g & 1) + 4 * p) * 2, wb1 = wb0 + 4 * 64;
-    f32x16 acc = {};
+    const int wb0 = (8 * (g >> 1) + q) * 64 + (16 * (g & 1) + 4 * p) * 2 + 1024 * mg;  // half hh: +256
+    f32x16 acc[4] = {};
     float bsum = 0.f;
 
     const int nmine = nframes > (int)blockIdx.x ? (nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
@@ -327,7 +336,7 @@ __global__ __launch_bounds__(512, 2) void conv1_wgrad_fr(const uint8_t* __restri
     };
     auto issue_dy = [&](int k) {
         const fi_i32x4 dr = make_rsrc(da1 + (size_t)(blockIdx.x + k * gridDim.x) * 12800, 25600);
-        const uint32_t base = lds0 + c1::RAW + (k & 1) * c1::OUT;
+        const uint32_t base = lds0 + c1::RAW + (k % 3) * c1::OUT;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int j = w + 8 * i;
@@ -335,14 +344,21 @@ __global__ __launch_bounds__(512, 2) void conv1_wgrad_fr(const uint8_t* __restri
         }
         return w == 0 ? 4 : 3;
     };
-    int issued = 0, mark = 0;
-    if (nmine > 0) { issued += issue_raw(0); issued += issue_dy(0); }
-    mark = issued;
-    if (nmine > 1) issued += issue_dy(1);
+    // issue order: raw(0) dy(0) dy(1) | per frame it: dy(it+2) after the first barrier,
+    // raw(it+1) after the second. mk_*: issue counts just after each frame's pieces.
+    int issued = 0, mk_raw = 0, mk_dy0 = 0, mk_dy1 = 0;
+    if (nmine > 0) { issued += issue_raw(0); mk_raw = issued; issued += issue_dy(0); mk_dy0 = issued; }
+    if (nmine > 1) { issued += issue_dy(1); mk_dy1 = issued; }
+    PH_DECL
     for (int it = 0; it < nmine; ++it) {
-        const char* dy = smem + c1::RAW + (it & 1) * c1::OUT;
-        wait_vmcnt(issued - mark);
-        lds_barrier();  // raw frame + da1 tile landed; image free
+        const char* dy = smem + c1::RAW + (it % 3) * c1::OUT;
+        PH(5);
+        wait_vmcnt(issued - max(mk_raw, mk_dy0));
+        PH(0);
+        lds_barrier();  // raw frame + da1 tile landed; previous frame consumed by every wave
+        PH(1);
+        int mk_dy2 = 0;
+        if (it + 2 < nmine) { issued += issue_dy(it + 2); mk_dy2 = issued; }
 #pragma unroll
         for (int i = 0; i < (c1::FRAME_LOADS + 511) / 512; ++i) {
             const int u = tid + 512 * i;
@@ -353,33 +369,82 @@ __global__ __launch_bounds__(512, 2) void conv1_wgrad_fr(const uint8_t* __restri
                 *(bf16x8*)(img + c1::PLANE + 16 * u) = hi;
             }
         }
+        PH(2);
         lds_barrier();  // image ready; raw slot free
-        if (it + 1 < nmine) issued += issue_raw(it + 1);
-        mark = issued;
+        PH(1);
+        if (it + 1 < nmine) { issued += issue_raw(it + 1); mk_raw = issued; }
+        PH(4);
+        const char* DB = dy + wb0;
+        auto load = [&](int j, bf16x8* d) {  // [0] da1, [1..4] A of k-tiles kt = 0..3
+            d[0] = tr2(DB + 4096 * j, DB + 256 + 4096 * j);
 #pragma unroll
-        for (int ms = 0; ms < 25; ++ms) {
-            const bf16x8 bfr = tr2(dy + wb0 + 1024 * ms, dy + wb1 + 1024 * ms);
-            if (w == 0) {
+            for (int kt = 0; kt < 4; ++kt) d[1 + kt] = tr2(img + wao[j][0] + 336 * kt, img + wao[j][1] + 336 * kt);
+        };
+        auto step = [&](const bf16x8* cur) {
+            if (kg == 0) {
 #pragma unroll
-                for (int j = 0; j < 8; ++j) bsum += (float)bfr[j];
+                for (int j = 0; j < 8; ++j) bsum += (float)cur[0][j];
             }
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr2(img + wao[ms][0], img + wao[ms][1]), bfr, acc, 0, 0, 0);
+#pragma unroll
+            for (int kt = 0; kt < 4; ++kt)
+                acc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[1 + kt], cur[0], acc[kt], 0, 0, 0);
+        };
+        bf16x8 fb[2][5];
+        load(0, fb[0]);
+        __builtin_amdgcn_sched_group_barrier(0x100, 10, 0);
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            if (j < 5) load(j + 1, fb[(j + 1) & 1]);
+            else if (mg == 0) load(6, fb[0]);  // m-group 0 also takes step 24
+            step(fb[j & 1]);
+#pragma unroll
+            for (int kt = 0; kt < 4; ++kt) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                if (j < 5) {
+                    if (kt < 2) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+                    else __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                }
+            }
         }
-        lds_barrier();  // image and da1 slot consumed
-        if (it + 2 < nmine) issued += issue_dy(it + 2);
+        if (mg == 0) step(fb[0]);
+        PH(3);
+        PH_ITER();
+        mk_dy0 = mk_dy1;
+        mk_dy1 = mk_dy2;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    // partial slab: rows k = 32w + (r&3) + 8(r>>2) + 4(lane>>5), col co = lane&31
+    PH_FLUSH();
+    // reduce the four m-groups in LDS (fixed order mg = 0..3), one k-group per round:
+    // red[mg][kt][r][lane] -> slab rows k = 32(4kg + kt) + (r&3) + 8(r>>2) + 4(lane>>5), col lane&31
+    float* red = (float*)smem;
     float* out = slab + (size_t)blockIdx.x * 256 * 32;
     const float inv255 = 1.0f / 255.0f;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int k = 32 * w + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        out[k * 32 + (lane & 31)] = acc[r] * inv255;
+    for (int round = 0; round < 2; ++round) {
+        __syncthreads();
+        if (kg == round) {
+#pragma unroll
+            for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) red[((mg * 4 + kt) * 16 + r) * 64 + lane] = acc[kt][r];
+        }
+        __syncthreads();
+        for (int e = tid; e < 4 * 16 * 64; e += 512) {  // e = (kt * 16 + r) * 64 + l
+            const float v = ((red[e] + red[4096 + e]) + red[8192 + e]) + red[12288 + e];
+            const int l = e & 63, r = (e >> 6) & 15, kt = e >> 10;
+            const int k = 32 * (4 * round + kt) + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
+            out[k * 32 + (l & 31)] = v * inv255;
+        }
     }
-    if (w == 0) {  // lanes l and l+32: same co = 16(g&1) + 4p + ... (tr column), other m half
-        const float o = __shfl_xor(bsum, 32, 64);
-        if (lane < 32) cs_slab[(size_t)blockIdx.x * 32 + lane] = bsum + o;
+    // bias partials: lanes l and l+32 hold the same co (tr column), other m half; the k-group 0
+    // waves hold disjoint m-steps -> [4][32] in LDS, summed in m-group order
+    __syncthreads();
+    const float o = bsum + __shfl_xor(bsum, 32, 64);
+    if (kg == 0 && lane < 32) red[32 * mg + lane] = o;
+    __syncthreads();
+    if (w == 0 && lane < 32) {
+        const float t = ((red[lane] + red[32 + lane]) + red[64 + lane]) + red[96 + lane];
+        cs_slab[(size_t)blockIdx.x * 32 + lane] = t;
     }
 }
 
@@ -388,6 +453,7 @@ int conv1_fwd_fr_launch(const uint8_t* frames, const __bf16* w1t, const float* b
     hipLaunchKernelGGL(conv1_fwd_fr, dim3(grid), dim3(512), 0, s, frames, w1t, bias, a1, nframes);
     FI_HIP_CHECK(hipGetLastError());
     st_report("conv1_fwd");
+    ph_report("conv1_fwd", grid);
     return FI_OK;
 }
 
@@ -395,6 +461,7 @@ int conv1_wgrad_fr_launch(const uint8_t* frames, const __bf16* da1, float* slab,
                           int nframes, int grid, hipStream_t s) {
     hipLaunchKernelGGL(conv1_wgrad_fr, dim3(grid), dim3(512), 0, s, frames, da1, slab, cs_slab, nframes);
     FI_HIP_CHECK(hipGetLastError());
+    ph_report("conv1_wgrad", grid);
     return FI_OK;
 }
 
