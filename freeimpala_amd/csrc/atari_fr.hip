@@ -468,59 +468,53 @@ int conv1_wgrad_fr_launch(const uint8_t* frames, const __bf16* da1, float* slab,
 
 // =====================================================================================
 // Frame-resident forward of conv2 (4x4/2, 32 -> 64) and conv3 (3x3/1, 64 -> 64).
-// 8 waves: wave w owns output channels 16*(w&3)..+16 (its weight slice stays in registers as
-// the MFMA A operand, so D = [channel][pixel] and a lane ends with 4 consecutive channels
-// of one pixel) and half of the frame's 16-pixel tiles. The input frame arrives by LDS-DMA
-// in a "chunk-planar" image: plane c holds the c-th 16-byte channel chunk of every pixel,
-// so the 16 lanes of an MFMA B-fragment read (16 consecutive output pixels, same chunk)
-// hit 16 consecutive LDS slots -- conflict-free. conv2 (stride 2) additionally splits each
-// plane into even then odd input pixels, which makes its stride-2 reads consecutive too.
-// Outputs (+bias, ReLU, bf16) are staged as [pixel][64] with the 16-byte chunk index
-// XOR-swizzled by the pixel, then leave as coalesced 16-byte stores.
+// 8 waves = 2 channel halves chh (32 output channels: two 16-channel A-operand tiles of the
+// weight slice in registers, so D = [channel][pixel]) x 4 pixel-tile groups pg; each B
+// fragment read feeds two MFMAs. A row i of channel tile ct is channel
+// 32chh + 8(i>>2) + 4ct + (i&3), so lane group g ends with channels 32chh + 8g..+8 of its
+// pixel and stores them straight from registers (16 B).
+// Output pixels are walked on an s-grid whose pitch equals the LDS image's row pitch
+// (conv2: s = 10oy + ox over the 10-wide parity-class planes; conv3: s = 9oy + ox over the
+// 9-wide image; the extra columns are computed and dropped), so a B read of tile pixels s
+// hits image units s + const: with chunk offsets Z(c) (chunks c, c+1 8 units apart) and the
+// tile lanes permuted (sig) every ds_read_b128 is conflict-free, and every fragment
+// address is a base register plus an immediate.
+//   conv2 image: unit = pos + 100 P + 416 c + Z(c), P = 2(iy&1) + (ix&1), pos = (iy>>1)*10 + (ix>>1)
+//   conv3 image: unit = p + 96 c + Z(c), p = 9 iy + ix
+// One barrier per iteration (FPI frames); the ring slot of the previous iteration takes the
+// DMA of iteration + RI - 1 right after it.
 // =====================================================================================
-namespace f2 {
-constexpr int NPIX = 400, PLANES = 4;        // a1: 20x20 pixels, 4 chunks of 8 channels
-constexpr int XB = NPIX * PLANES * 16;       // 25,600
-constexpr int NX = XB / 1024;                // 25 pieces
-constexpr int OUTT = 81 * 128;               // a2 tile [81][64] bf16 (swizzled chunks)
-constexpr int OUT_CH = 81 * 8;               // 648
-}  // namespace f2
-namespace f3 {
-constexpr int NPIX = 81, PLANES = 8;         // a2: 9x9 pixels, 8 chunks of 8 channels
-constexpr int XB = 11 * 1024;                // 648 slots = 10,368 B, 11 pieces (tail reads zeros)
-constexpr int NX = 11;
-constexpr int OUTT = 49 * 128;               // a3 tile [49][64] bf16 (swizzled chunks)
-constexpr int OUT_CH = 49 * 8;               // 392
-}  // namespace f3
+__host__ __device__ constexpr int fz(int c) { return 8 * (c & 1) + 4 * ((c >> 1) & 1); }
 
-// LDS slot s of the conv2 input image -> byte offset of its 16-byte chunk in the a1 frame
-__device__ __forceinline__ uint32_t f2_src(int s) {
-    const int c = s / f2::NPIX, r = s - c * f2::NPIX;
-    const int p = r < f2::NPIX / 2 ? 2 * r : 2 * (r - f2::NPIX / 2) + 1;
-    return (uint32_t)(64 * p + 16 * c);
+// LDS unit u of the conv2 input image -> byte offset of its 16-byte chunk in the a1 frame
+__device__ __forceinline__ uint32_t f2_src(int u) {
+    const int c = u / 416, k = u - 416 * c - fz(c);
+    if (c >= 4 || k < 0 || k >= 400) return FI_OOB;
+    const int P = k / 100, pos = k - 100 * P, py = pos / 10, px = pos - 10 * py;
+    return (uint32_t)(((2 * py + (P >> 1)) * 20 + 2 * px + (P & 1)) * 64 + 16 * c);
 }
-__device__ __forceinline__ uint32_t f3_src(int s) {
-    const int c = s / f3::NPIX, p = s - c * f3::NPIX;
-    return s < f3::NPIX * f3::PLANES ? (uint32_t)(128 * p + 16 * c) : FI_OOB;
+__device__ __forceinline__ uint32_t f3_src(int u) {
+    const int c = u / 96, k = u - 96 * c - fz(c);
+    return c < 8 && k >= 0 && k <= 80 ? (uint32_t)(128 * k + 16 * c) : FI_OOB;
 }
 
 template <int L>  // L = 2 (conv2) or 3 (conv3)
 struct FwdGeo;
 template <>
 struct FwdGeo<2> {  // two frames per iteration: 12 pixel tiles = 4 groups x 3
-    static constexpr int XB = f2::XB, NX = f2::NX, OUTT = f2::OUTT, OUT_CH = f2::OUT_CH;
-    static constexpr int IN_BYTES = 25600, OUT_ELEMS = 5184, IN_ELEMS = 12800, KS = 16, NT = 6, OPIX = 81;
+    static constexpr int NX = 27, XB = NX * 1024;  // 1,680 used units
+    static constexpr int IN_BYTES = 25600, OUT_ELEMS = 5184, IN_ELEMS = 12800, KS = 16, NT = 6;
+    static constexpr int SW = 10, OW = 9;  // s-grid pitch, output width (= height)
     static constexpr int FPI = 2, RING_I = 2;
 };
 template <>
 struct FwdGeo<3> {  // one frame per iteration: 4 pixel tiles = 4 groups x 1
-    static constexpr int XB = f3::XB, NX = f3::NX, OUTT = f3::OUTT, OUT_CH = f3::OUT_CH;
-    static constexpr int IN_BYTES = 10368, OUT_ELEMS = 3136, IN_ELEMS = 5184, KS = 18, NT = 4, OPIX = 49;
-    static constexpr int FPI = 1, RING_I = 3;
+    static constexpr int NX = 12, XB = NX * 1024;  // 768 units
+    static constexpr int IN_BYTES = 10368, OUT_ELEMS = 3136, IN_ELEMS = 5184, KS = 18, NT = 4;
+    static constexpr int SW = 9, OW = 7;
+    static constexpr int FPI = 1, RING_I = 4;
 };
 
-// 8 waves = 2 channel halves (32 channels, two 16-channel A-operand tiles in registers) x 4
-// pixel-tile groups: each B fragment read from LDS feeds two MFMAs.
 template <int L>
 __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__ x,    // NHWC input frames
                                                       const __bf16* __restrict__ wt,   // [64][K] (ky,kx,ci)
@@ -530,46 +524,36 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
     using G = FwdGeo<L>;
     constexpr int K = G::KS * 32, FPI = G::FPI, RI = G::RING_I;
     constexpr int TPW = G::NT * FPI / 4;  // pixel tiles per wave
-    __shared__ __attribute__((aligned(16))) char smem[RI * FPI * G::XB + FPI * G::OUTT + G::NX * 64 * 4];
+    __shared__ __attribute__((aligned(16))) char smem[RI * FPI * G::XB + G::NX * 64 * 4];
     const int lane = threadIdx.x & 63, tid = threadIdx.x;
     const int w = wave_id(), chh = w >> 2, pg = w & 3;
-    const int g = lane >> 4, c16 = lane & 15;
+    const int g = lane >> 4, c16 = lane & 15, si = c16 ^ ((c16 >> 1) & 4);
     const uint32_t lds0 = lds_addr(smem);
-    char* outt = smem + RI * FPI * G::XB;
-    uint32_t* srcs = (uint32_t*)(smem + RI * FPI * G::XB + FPI * G::OUTT);  // DMA gather table
+    uint32_t* srcs = (uint32_t*)(smem + RI * FPI * G::XB);  // DMA gather table
     for (int i = tid; i < G::NX * 64; i += 512) srcs[i] = L == 2 ? f2_src(i) : f3_src(i);
 
-    // A operand (weights): lane holds W[co = 32chh + 16ct + c16][k = 32ks + 8g..+8], ct = 0, 1
+    // A operand: lane holds W[co = 32chh + 8(i>>2) + 4ct + (i&3), i = c16][k = 32ks + 8g..+8]
     bf16x8 wa[2][G::KS];
 #pragma unroll
     for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
         for (int ks = 0; ks < G::KS; ++ks)
-            wa[ct][ks] = *(const bf16x8*)(wt + (size_t)(32 * chh + 16 * ct + c16) * K + 32 * ks + 8 * g);
-    float bch[2][4];
+            wa[ct][ks] = *(const bf16x8*)(wt + (size_t)(32 * chh + 8 * (c16 >> 2) + 4 * ct + (c16 & 3)) * K +
+                                          32 * ks + 8 * g);
+    float bch[8];  // bias of the lane's channels 32chh + 8g + j
 #pragma unroll
-    for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) bch[ct][r] = bias[32 * chh + 16 * ct + 4 * g + r];
-    // this wave's pixel tiles: global tile t = TPW*pg + i over the FPI frames of an iteration
+    for (int j = 0; j < 8; ++j) bch[j] = bias[32 * chh + 8 * g + j];
+    // this wave's tiles: global tile t = TPW*pg + i over the FPI frames of an iteration;
+    // lane pixel s = 16 tt + sig(c16) of frame fi; B unit = s + chunk offset + tap immediate
     int bbase[TPW];
 #pragma unroll
     for (int i = 0; i < TPW; ++i) {
-        const int t = TPW * pg + i, fi = t / G::NT, tt = t - fi * G::NT;
-        const int n = min(16 * tt + c16, G::OPIX - 1);
-        if (L == 2) {
-            const int oy = n / 9, ox = n - 9 * oy;  // input pixel (2oy+ky, 2ox+kx), even/odd split
-            bbase[i] = fi * G::XB + 16 * (f2::NPIX * g + 20 * oy + ox);
-        } else {
-            const int oy = n / 7, ox = n - 7 * oy;  // input pixel (oy+ky, ox+kx)
-            bbase[i] = fi * G::XB + 16 * (f3::NPIX * g + 9 * oy + ox);
-        }
+        const int t = TPW * pg + i, fi = t / G::NT, tt = t - fi * G::NT, s = 16 * tt + si;
+        bbase[i] = fi * G::XB + 16 * (s + (L == 2 ? 416 : 96) * g + fz(g));
     }
     __syncthreads();  // gather table ready
 
     const int npw = (G::NX - w + 7) / 8;  // pieces per frame issued by this wave
-    // copy-out store instructions per frame issued by this wave (lower bound: safe to count)
-    const int nst = G::OUT_CH / 512 + (G::OUT_CH % 512 > 64 * w ? 1 : 0);
     const int nmine = nframes > (int)blockIdx.x ? (nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
     const int niter = (nmine + FPI - 1) / FPI;
     // queue the frames of iteration i2 into ring slot (i2 % RI); returns the pieces issued
@@ -582,10 +566,16 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
                 const int f = blockIdx.x + k * gridDim.x;
                 const fi_i32x4 xr = make_rsrc(x + (size_t)f * G::IN_ELEMS, G::IN_BYTES);
                 const uint32_t slot_lds = lds0 + ((i2 % RI) * FPI + u) * G::XB;
+                uint32_t o[(G::NX + 7) / 8];
 #pragma unroll
                 for (int i = 0; i < (G::NX + 7) / 8; ++i) {
                     const int j = w + 8 * i;
-                    if (j < G::NX) blds16(xr, srcs[64 * j + lane], slot_lds + 1024 * j);
+                    o[i] = j < G::NX ? srcs[64 * j + lane] : 0u;
+                }
+#pragma unroll
+                for (int i = 0; i < (G::NX + 7) / 8; ++i) {
+                    const int j = w + 8 * i;
+                    if (j < G::NX) blds16(xr, o[i], slot_lds + 1024 * j);
                 }
                 n += npw;
             }
@@ -594,88 +584,98 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
     };
     ST_DECL
     ST();
-    int issued = 0, mk[RI];
+    int issued = 0, mk[RI - 1];
 #pragma unroll
-    for (int i = 0; i < RI; ++i) {
+    for (int i = 0; i < RI - 1; ++i) {
         if (i < niter) issued += issue(i);
         mk[i] = issued;
     }
+    PH_DECL
     for (int it = 0; it < niter; ++it) {
         const char* X = smem + (it % RI) * FPI * G::XB;
+        PH(5);
         wait_vmcnt(issued - mk[0]);
-        lds_barrier();  // frames landed; previous out tiles drained
+        PH(0);
+        lds_barrier();  // frames of iteration it landed; iteration it-1 consumed by every wave
+        PH(1);
         if (it < 5) ST();
+        int mnew = 0;
+        if (it + RI - 1 < niter) {
+            issued += issue(it + RI - 1);
+            mnew = issued;
+        }
+        PH(2);
         f32x4 acc[TPW][2];
 #pragma unroll
         for (int i = 0; i < TPW; ++i) { acc[i][0] = f32x4{}; acc[i][1] = f32x4{}; }
+        auto imm = [&](int ks) {
+            if (L == 2) {  // tap = ks (32 channels = chunks 0..3): class plane + position shift
+                const int ky = ks >> 2, kx = ks & 3;
+                return 16 * (10 * (ky >> 1) + (kx >> 1) + 100 * (2 * (ky & 1) + (kx & 1)));
+            } else {       // tap = ks/2, channel half ks&1 -> chunk + 4
+                const int tap = ks >> 1, ky = tap / 3, kx = tap - 3 * ky;
+                return 16 * (9 * ky + kx + 384 * (ks & 1));
+            }
+        };
+        // software pipeline: step ks+PD's fragments are read between step ks's MFMAs
+        constexpr int PD = TPW >= 3 ? 1 : 3;
+        bf16x8 fb[PD + 1][TPW];
+#pragma unroll
+        for (int ks = 0; ks < PD; ++ks)
+#pragma unroll
+            for (int i = 0; i < TPW; ++i) fb[ks][i] = *(const bf16x8*)(X + bbase[i] + imm(ks));
+        __builtin_amdgcn_sched_group_barrier(0x100, PD * TPW, 0);
 #pragma unroll
         for (int ks = 0; ks < G::KS; ++ks) {
-            int imm;
-            if (L == 2) {  // tap = ks (32 channels); kx parity selects the odd-pixel half
-                const int ky = ks >> 2, kx = ks & 3;
-                imm = 16 * (10 * ky + (kx >> 1) + (f2::NPIX / 2) * (kx & 1));
-            } else {       // tap = ks/2, channel half ks&1 -> planes 4(ks&1) + g
-                const int tap = ks >> 1, ky = tap / 3, kx = tap - 3 * ky;
-                imm = 16 * (f3::NPIX * 4 * (ks & 1) + 9 * ky + kx);
+            if (ks + PD < G::KS) {
+#pragma unroll
+                for (int i = 0; i < TPW; ++i) fb[(ks + PD) % (PD + 1)][i] = *(const bf16x8*)(X + bbase[i] + imm(ks + PD));
             }
 #pragma unroll
             for (int i = 0; i < TPW; ++i) {
-                const bf16x8 b = *(const bf16x8*)(X + bbase[i] + imm);
+                const bf16x8 b = fb[ks % (PD + 1)][i];
                 acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[0][ks], b, acc[i][0], 0, 0, 0);
                 acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[1][ks], b, acc[i][1], 0, 0, 0);
             }
+#pragma unroll
+            for (int i = 0; i < TPW; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                if (ks + PD < G::KS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            }
         }
-        if (it < 5) ST();
+        PH(3);
+        // epilogue: one 16-byte store per tile (its frame present), lanes on dropped s masked
+        int nst = 0;
 #pragma unroll
         for (int i = 0; i < TPW; ++i) {
-            const int t = TPW * pg + i, fi = t / G::NT, tt = t - fi * G::NT;
-            const int n = 16 * tt + c16;
-            if (n < G::OPIX) {
+            const int t = TPW * pg + i, fi = t / G::NT, tt = t - fi * G::NT, s = 16 * tt + si;
+            const int k = FPI * it + fi;
+            if (k < nmine) {
+                ++nst;
+                const int oy = s / G::SW, ox = s - G::SW * oy;
+                if (oy < G::OW && ox < G::OW) {
+                    bf16x8 o;
 #pragma unroll
-                for (int ct = 0; ct < 2; ++ct) {
-                    bf16x4 o;
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) o[r] = (__bf16)fmaxf(acc[i][ct][r] + bch[ct][r], 0.f);
-                    const int chunk = (4 * chh + 2 * ct + (g >> 1)) ^ (n & 7);
-                    *(bf16x4*)(outt + fi * G::OUTT + 128 * n + 16 * chunk + 8 * (g & 1)) = o;
-                }
-            }
-        }
-        lds_barrier();  // out tiles complete
-        if (it < 5) ST();
-        {
-#pragma unroll
-            for (int u = 0; u < FPI; ++u) {
-                const int k = FPI * it + u;
-                if (k < nmine) {
-                    issued += nst;
-                    u32x4* dst = (u32x4*)(y + (size_t)(blockIdx.x + k * gridDim.x) * G::OUT_ELEMS);
-#pragma unroll
-                    for (int i = 0; i < (G::OUT_CH + 511) / 512; ++i) {
-                        const int P = tid + 512 * i;
-                        if (P < G::OUT_CH) {
-                            const int n = P >> 3, c = P & 7;
-                            FI_ST16(*(const u32x4*)(outt + u * G::OUTT + 128 * n + 16 * (c ^ (n & 7))), dst + P);
-                        }
+                    for (int r = 0; r < 4; ++r) {
+                        o[r] = (__bf16)fmaxf(acc[i][0][r] + bch[r], 0.f);
+                        o[4 + r] = (__bf16)fmaxf(acc[i][1][r] + bch[4 + r], 0.f);
                     }
+                    u32x4* dst = (u32x4*)(y + (size_t)(blockIdx.x + k * gridDim.x) * G::OUT_ELEMS);
+                    FI_ST16(__builtin_bit_cast(u32x4, o), dst + 8 * (G::OW * oy + ox) + 4 * chh + g);
                 }
             }
         }
-        lds_barrier();  // ring slot consumed
-        if (it < 5) ST();
-        int mnew = issued;  // (a later wait on this mark never waits for the stores above)
-        if (it + RI < niter) {
-            issued += issue(it + RI);
-            mnew = issued;
-        }
+        issued += nst;
+        PH(4);
+        PH_ITER();
 #pragma unroll
-        for (int i = 0; i + 1 < RI; ++i) mk[i] = mk[i + 1];
-        mk[RI - 1] = mnew;
-        if (it < 5) ST();
+        for (int i = 0; i + 1 < RI - 1; ++i) mk[i] = mk[i + 1];
+        mk[RI - 2] = mnew;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     ST();
     ST_FLUSH();
+    PH_FLUSH();
 }
 
 int conv2_fwd_fr_launch(const __bf16* a1, const __bf16* w2t, const float* bias, __bf16* a2, int nframes,
@@ -683,6 +683,7 @@ int conv2_fwd_fr_launch(const __bf16* a1, const __bf16* w2t, const float* bias, 
     hipLaunchKernelGGL(conv_fwd_fr<2>, dim3(grid), dim3(512), 0, s, a1, w2t, bias, a2, nframes);
     FI_HIP_CHECK(hipGetLastError());
     st_report("conv2_fwd");
+    ph_report("conv2_fwd", grid);
     return FI_OK;
 }
 
@@ -691,6 +692,7 @@ int conv3_fwd_fr_launch(const __bf16* a2, const __bf16* w3t, const float* bias, 
     hipLaunchKernelGGL(conv_fwd_fr<3>, dim3(grid), dim3(512), 0, s, a2, w3t, bias, a3, nframes);
     FI_HIP_CHECK(hipGetLastError());
     st_report("conv3_fwd");
+    ph_report("conv3_fwd", grid);
     return FI_OK;
 }
 
