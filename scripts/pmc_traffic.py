@@ -23,6 +23,8 @@ TAGS = {
     "conv3_bwd": "conv3_bwd_fr",
     "conv1_fwd": "conv1_fwd_fr",
     "conv1_wgrad": "conv1_wgrad_fr",
+    "conv2_fwd": "conv_fwd_fr<2>",
+    "conv3_fwd": "conv_fwd_fr<3>",
 }
 
 
