@@ -17,6 +17,8 @@
 //   plane h, slot (4oy+ky)*21 + ox + (ks&1): consecutive output pixels hit consecutive
 //   16-byte slots (including across output-row wraps: 4*21 - 19 = 65 = 1 mod 16), so
 //   ds_read_b128 is bank-conflict free.
+#include <type_traits>
+
 #include "atari.h"
 #include "fi_common.h"
 #include "kernels.h"
@@ -481,38 +483,39 @@ int conv1_wgrad_fr_launch(const uint8_t* frames, const __bf16* da1, float* slab,
 // address is a base register plus an immediate.
 //   conv2 image: unit = pos + 100 P + 416 c + Z(c), P = 2(iy&1) + (ix&1), pos = (iy>>1)*10 + (ix>>1)
 //   conv3 image: unit = p + 96 c + Z(c), p = 9 iy + ix
-// One barrier per iteration (FPI frames); the ring slot of the previous iteration takes the
-// DMA of iteration + RI - 1 right after it.
+// Input frames arrive by LDS-DMA in their own byte order (1 KiB contiguous per wave
+// instruction: a gather straight into the chunk-planar image cost ~15% of conv2's kernel in
+// memory requests) into STG staging buffers, and each issuing wave moves its own landed
+// pieces into the other of two image slots (ds_read/ds_write_b128) after the iteration's
+// MFMAs, behind a counted vmcnt that lets the output stores fly. One barrier per iteration.
 // =====================================================================================
 __host__ __device__ constexpr int fz(int c) { return 8 * (c & 1) + 4 * ((c >> 1) & 1); }
 
-// LDS unit u of the conv2 input image -> byte offset of its 16-byte chunk in the a1 frame
-__device__ __forceinline__ uint32_t f2_src(int u) {
-    const int c = u / 416, k = u - 416 * c - fz(c);
-    if (c >= 4 || k < 0 || k >= 400) return FI_OOB;
-    const int P = k / 100, pos = k - 100 * P, py = pos / 10, px = pos - 10 * py;
-    return (uint32_t)(((2 * py + (P >> 1)) * 20 + 2 * px + (P & 1)) * 64 + 16 * c);
+// 16-byte unit i of an input frame (pixel i/4 or i/8, chunk i%4 or i%8) -> image unit
+__device__ __forceinline__ int f2_dst(int i) {
+    const int p = i >> 2, c = i & 3, iy = p / 20, ix = p - 20 * iy;
+    return ((iy >> 1) * 10 + (ix >> 1)) + 100 * (2 * (iy & 1) + (ix & 1)) + 416 * c + fz(c);
 }
-__device__ __forceinline__ uint32_t f3_src(int u) {
-    const int c = u / 96, k = u - 96 * c - fz(c);
-    return c < 8 && k >= 0 && k <= 80 ? (uint32_t)(128 * k + 16 * c) : FI_OOB;
+__device__ __forceinline__ int f3_dst(int i) {
+    const int p = i >> 3, c = i & 7;
+    return p < 81 ? p + 96 * c + fz(c) : 0;
 }
 
 template <int L>  // L = 2 (conv2) or 3 (conv3)
 struct FwdGeo;
 template <>
 struct FwdGeo<2> {  // two frames per iteration: 12 pixel tiles = 4 groups x 3
-    static constexpr int NX = 27, XB = NX * 1024;  // 1,680 used units
+    static constexpr int XB = 1680 * 16;           // image units per frame
     static constexpr int IN_BYTES = 25600, OUT_ELEMS = 5184, IN_ELEMS = 12800, KS = 16, NT = 6;
     static constexpr int SW = 10, OW = 9;  // s-grid pitch, output width (= height)
-    static constexpr int FPI = 2, RING_I = 2;
+    static constexpr int FPI = 2, STG = 1;  // frames per iteration, staging buffers (iterations ahead)
 };
 template <>
-struct FwdGeo<3> {  // one frame per iteration: 4 pixel tiles = 4 groups x 1
-    static constexpr int NX = 12, XB = NX * 1024;  // 768 units
+struct FwdGeo<3> {  // two frames per iteration: 8 pixel tiles = 4 groups x 2
+    static constexpr int XB = 768 * 16;
     static constexpr int IN_BYTES = 10368, OUT_ELEMS = 3136, IN_ELEMS = 5184, KS = 18, NT = 4;
     static constexpr int SW = 9, OW = 7;
-    static constexpr int FPI = 1, RING_I = 4;
+    static constexpr int FPI = 2, STG = 2;
 };
 
 template <int L>
@@ -522,15 +525,20 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
                                                       __bf16* __restrict__ y,          // NHWC output frames
                                                       int nframes) {
     using G = FwdGeo<L>;
-    constexpr int K = G::KS * 32, FPI = G::FPI, RI = G::RING_I;
-    constexpr int TPW = G::NT * FPI / 4;  // pixel tiles per wave
-    __shared__ __attribute__((aligned(16))) char smem[RI * FPI * G::XB + G::NX * 64 * 4];
+    constexpr int K = G::KS * 32, FPI = G::FPI, STG = G::STG;
+    constexpr int TPW = G::NT * FPI / 4;                // pixel tiles per wave
+    constexpr int NLP = (G::IN_BYTES + 1023) / 1024;   // 1-KiB pieces per input frame
+    constexpr int PPW = (NLP + 7) / 8;                  // pieces per wave per frame (at most)
+    constexpr int IMG = 2 * FPI * G::XB, SBUF = FPI * NLP * 1024;
+    __shared__ __attribute__((aligned(16))) char smem[IMG + STG * SBUF + NLP * 64 * 2];
     const int lane = threadIdx.x & 63, tid = threadIdx.x;
     const int w = wave_id(), chh = w >> 2, pg = w & 3;
     const int g = lane >> 4, c16 = lane & 15, si = c16 ^ ((c16 >> 1) & 4);
     const uint32_t lds0 = lds_addr(smem);
-    uint32_t* srcs = (uint32_t*)(smem + RI * FPI * G::XB);  // DMA gather table
-    for (int i = tid; i < G::NX * 64; i += 512) srcs[i] = L == 2 ? f2_src(i) : f3_src(i);
+    // image unit of every 16-byte unit of the input frame
+    uint16_t* dstu = (uint16_t*)(smem + IMG + STG * SBUF);
+    for (int i = tid; i < NLP * 64; i += 512) dstu[i] = (uint16_t)(L == 2 ? f2_dst(i) : f3_dst(i));
+    for (int i = tid; i < IMG / 16; i += 512) ((u32x4*)smem)[i] = u32x4{0, 0, 0, 0};  // gap units
 
     // A operand: lane holds W[co = 32chh + 8(i>>2) + 4ct + (i&3), i = c16][k = 32ks + 8g..+8]
     bf16x8 wa[2][G::KS];
@@ -551,126 +559,145 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
         const int t = TPW * pg + i, fi = t / G::NT, tt = t - fi * G::NT, s = 16 * tt + si;
         bbase[i] = fi * G::XB + 16 * (s + (L == 2 ? 416 : 96) * g + fz(g));
     }
-    __syncthreads();  // gather table ready
-
-    const int npw = (G::NX - w + 7) / 8;  // pieces per frame issued by this wave
     const int nmine = nframes > (int)blockIdx.x ? (nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
     const int niter = (nmine + FPI - 1) / FPI;
-    // queue the frames of iteration i2 into ring slot (i2 % RI); returns the pieces issued
+    // iteration i2's frames: wave w DMAs pieces j = w + 8i of each frame, in the frame's own
+    // byte order (fully coalesced), into staging buffer i2 % STG; returns the pieces issued
     auto issue = [&](int i2) {
         int n = 0;
 #pragma unroll
         for (int u = 0; u < FPI; ++u) {
             const int k = FPI * i2 + u;
             if (k < nmine) {
-                const int f = blockIdx.x + k * gridDim.x;
-                const fi_i32x4 xr = make_rsrc(x + (size_t)f * G::IN_ELEMS, G::IN_BYTES);
-                const uint32_t slot_lds = lds0 + ((i2 % RI) * FPI + u) * G::XB;
-                uint32_t o[(G::NX + 7) / 8];
+                const fi_i32x4 xr = make_rsrc(x + (size_t)(blockIdx.x + k * gridDim.x) * G::IN_ELEMS, G::IN_BYTES);
+                const uint32_t sb = lds0 + IMG + (i2 % STG) * SBUF + u * NLP * 1024;
 #pragma unroll
-                for (int i = 0; i < (G::NX + 7) / 8; ++i) {
+                for (int i = 0; i < PPW; ++i) {
                     const int j = w + 8 * i;
-                    o[i] = j < G::NX ? srcs[64 * j + lane] : 0u;
+                    if (j < NLP) {
+                        blds16(xr, 1024 * j + 16 * lane, sb + 1024 * j);
+                        ++n;
+                    }
                 }
-#pragma unroll
-                for (int i = 0; i < (G::NX + 7) / 8; ++i) {
-                    const int j = w + 8 * i;
-                    if (j < G::NX) blds16(xr, o[i], slot_lds + 1024 * j);
-                }
-                n += npw;
             }
         }
         return n;
     };
-    ST_DECL
-    ST();
-    int issued = 0, mk[RI - 1];
+    // the issuing wave moves its own landed pieces of iteration i2 into image slot i2 & 1
+    // (all reads first, then all writes: one LDS round trip, not one per piece)
+    auto reshuffle = [&](int i2) {
+        u32x4 d[FPI][PPW];
+        int du[FPI][PPW];
 #pragma unroll
-    for (int i = 0; i < RI - 1; ++i) {
-        if (i < niter) issued += issue(i);
-        mk[i] = issued;
-    }
-    PH_DECL
-    for (int it = 0; it < niter; ++it) {
-        const char* X = smem + (it % RI) * FPI * G::XB;
-        PH(5);
-        wait_vmcnt(issued - mk[0]);
-        PH(0);
-        lds_barrier();  // frames of iteration it landed; iteration it-1 consumed by every wave
-        PH(1);
-        if (it < 5) ST();
-        int mnew = 0;
-        if (it + RI - 1 < niter) {
-            issued += issue(it + RI - 1);
-            mnew = issued;
-        }
-        PH(2);
-        f32x4 acc[TPW][2];
+        for (int u = 0; u < FPI; ++u)
 #pragma unroll
-        for (int i = 0; i < TPW; ++i) { acc[i][0] = f32x4{}; acc[i][1] = f32x4{}; }
-        auto imm = [&](int ks) {
-            if (L == 2) {  // tap = ks (32 channels = chunks 0..3): class plane + position shift
-                const int ky = ks >> 2, kx = ks & 3;
-                return 16 * (10 * (ky >> 1) + (kx >> 1) + 100 * (2 * (ky & 1) + (kx & 1)));
-            } else {       // tap = ks/2, channel half ks&1 -> chunk + 4
-                const int tap = ks >> 1, ky = tap / 3, kx = tap - 3 * ky;
-                return 16 * (9 * ky + kx + 384 * (ks & 1));
-            }
-        };
-        // software pipeline: step ks+PD's fragments are read between step ks's MFMAs
-        constexpr int PD = TPW >= 3 ? 1 : 3;
-        bf16x8 fb[PD + 1][TPW];
-#pragma unroll
-        for (int ks = 0; ks < PD; ++ks)
-#pragma unroll
-            for (int i = 0; i < TPW; ++i) fb[ks][i] = *(const bf16x8*)(X + bbase[i] + imm(ks));
-        __builtin_amdgcn_sched_group_barrier(0x100, PD * TPW, 0);
-#pragma unroll
-        for (int ks = 0; ks < G::KS; ++ks) {
-            if (ks + PD < G::KS) {
-#pragma unroll
-                for (int i = 0; i < TPW; ++i) fb[(ks + PD) % (PD + 1)][i] = *(const bf16x8*)(X + bbase[i] + imm(ks + PD));
+            for (int i = 0; i < PPW; ++i) {
+                const int j = min(w + 8 * i, NLP - 1);
+                d[u][i] = *(const u32x4*)(smem + IMG + (i2 % STG) * SBUF + u * NLP * 1024 + 1024 * j + 16 * lane);
+                du[u][i] = dstu[64 * j + lane];
             }
 #pragma unroll
-            for (int i = 0; i < TPW; ++i) {
-                const bf16x8 b = fb[ks % (PD + 1)][i];
-                acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[0][ks], b, acc[i][0], 0, 0, 0);
-                acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[1][ks], b, acc[i][1], 0, 0, 0);
-            }
-#pragma unroll
-            for (int i = 0; i < TPW; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-                if (ks + PD < G::KS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-            }
-        }
-        PH(3);
-        // epilogue: one 16-byte store per tile (its frame present), lanes on dropped s masked
-        int nst = 0;
-#pragma unroll
-        for (int i = 0; i < TPW; ++i) {
-            const int t = TPW * pg + i, fi = t / G::NT, tt = t - fi * G::NT, s = 16 * tt + si;
-            const int k = FPI * it + fi;
+        for (int u = 0; u < FPI; ++u) {
+            const int k = FPI * i2 + u;
             if (k < nmine) {
-                ++nst;
-                const int oy = s / G::SW, ox = s - G::SW * oy;
-                if (oy < G::OW && ox < G::OW) {
-                    bf16x8 o;
+                char* im = smem + ((i2 & 1) * FPI + u) * G::XB;
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        o[r] = (__bf16)fmaxf(acc[i][0][r] + bch[r], 0.f);
-                        o[4 + r] = (__bf16)fmaxf(acc[i][1][r] + bch[4 + r], 0.f);
-                    }
-                    u32x4* dst = (u32x4*)(y + (size_t)(blockIdx.x + k * gridDim.x) * G::OUT_ELEMS);
-                    FI_ST16(__builtin_bit_cast(u32x4, o), dst + 8 * (G::OW * oy + ox) + 4 * chh + g);
+                for (int i = 0; i < PPW; ++i) {
+                    const int j = w + 8 * i, b = 1024 * j + 16 * lane;
+                    if (j < NLP && b < G::IN_BYTES) *(u32x4*)(im + 16 * du[u][i]) = d[u][i];
                 }
             }
         }
-        issued += nst;
+    };
+    __syncthreads();  // table and zeroed image ready
+    // issue order: DMA(0), then per iteration: stores, DMA(it + 1 + STG) after reshuffle(it + 1).
+    // mk[q]: issue count right after DMA(it + 1 + q), q < STG
+    int issued = 0, mk[STG];
+    if (niter > 0) {
+        issued += issue(0);
+        wait_vmcnt(0);
+        reshuffle(0);
+    }
+#pragma unroll
+    for (int q = 0; q < STG; ++q) {
+        if (1 + q < niter) issued += issue(1 + q);
+        mk[q] = issued;
+    }
+    auto imm = [&](int ks) {
+        if (L == 2) {  // tap = ks (32 channels = chunks 0..3): class plane + position shift
+            const int ky = ks >> 2, kx = ks & 3;
+            return 16 * (10 * (ky >> 1) + (kx >> 1) + 100 * (2 * (ky & 1) + (kx & 1)));
+        } else {       // tap = ks/2, channel half ks&1 -> chunk + 4
+            const int tap = ks >> 1, ky = tap / 3, kx = tap - 3 * ky;
+            return 16 * (9 * ky + kx + 384 * (ks & 1));
+        }
+    };
+    constexpr int NSTEP = TPW * G::KS;  // (tile, k-step) steps per iteration
+    ST_DECL
+    ST();
+    PH_DECL
+    for (int it = 0; it < niter; ++it) {
+        const char* X = smem + (it & 1) * FPI * G::XB;
+        PH(5);
+        lds_barrier();  // iteration it's image written; iteration it-1 consumed by every wave
+        PH(1);
+        if (it < 5) ST();
+        // tile-outer steps: each tile's 2*KS MFMAs end in its 16-byte store; B fragments are
+        // read PD steps ahead of their MFMAs
+        constexpr int PD = 4;
+        bf16x8 fb[PD + 1];
+#pragma unroll
+        for (int st = 0; st < PD; ++st) fb[st] = *(const bf16x8*)(X + bbase[st / G::KS] + imm(st % G::KS));
+        __builtin_amdgcn_sched_group_barrier(0x100, PD, 0);
+        f32x4 acc0 = f32x4{}, acc1 = f32x4{};
+#pragma unroll
+        for (int st = 0; st < NSTEP; ++st) {
+            const int i = st / G::KS, ks = st % G::KS;
+            if (st + PD < NSTEP)
+                fb[(st + PD) % (PD + 1)] = *(const bf16x8*)(X + bbase[(st + PD) / G::KS] + imm((st + PD) % G::KS));
+            const bf16x8 b = fb[st % (PD + 1)];
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[0][ks], b, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[1][ks], b, acc1, 0, 0, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+            if (st + PD < NSTEP) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            if (ks == G::KS - 1) {  // tile i done: bias, ReLU, one 16-byte store (its frame present)
+                const int t = TPW * pg + i, fi = t / G::NT, tt = t - fi * G::NT, s = 16 * tt + si;
+                const int k = FPI * it + fi;
+                if (k < nmine) {
+                    ++issued;
+                    const int oy = s / G::SW, ox = s - G::SW * oy;
+                    if (oy < G::OW && ox < G::OW) {
+                        bf16x8 ov;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            ov[r] = (__bf16)fmaxf(acc0[r] + bch[r], 0.f);
+                            ov[4 + r] = (__bf16)fmaxf(acc1[r] + bch[4 + r], 0.f);
+                        }
+                        u32x4* dst = (u32x4*)(y + (size_t)(blockIdx.x + k * gridDim.x) * G::OUT_ELEMS);
+                        FI_ST16(__builtin_bit_cast(u32x4, ov), dst + 8 * (G::OW * oy + ox) + 4 * chh + g);
+                    }
+                }
+                acc0 = f32x4{};
+                acc1 = f32x4{};
+            }
+        }
+        PH(3);
+        if (it + 1 < niter) {
+            wait_vmcnt(issued - mk[0]);  // own pieces of iteration it + 1 landed (stores may fly)
+            PH(0);
+            reshuffle(it + 1);           // image slot (it+1)&1 was last read in iteration it-1
+        }
+        PH(2);
+        int mnew = issued;
+        if (it + 1 + STG < niter) {
+            issued += issue(it + 1 + STG);  // into the staging buffer just emptied
+            mnew = issued;
+        }
+#pragma unroll
+        for (int q = 0; q + 1 < STG; ++q) mk[q] = mk[q + 1];
+        mk[STG - 1] = mnew;
         PH(4);
         PH_ITER();
-#pragma unroll
-        for (int i = 0; i + 1 < RI - 1; ++i) mk[i] = mk[i + 1];
-        mk[RI - 2] = mnew;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     ST();
@@ -789,7 +816,11 @@ __device__ __forceinline__ void c2_frames(const C2Ctx& c, char* smem, int nst, W
     const uint32_t lds0 = lds_addr(smem);
     // per-unit source offsets of both gathers (FI_OOB for border / gap units)
     uint32_t* tab = (uint32_t*)(smem + c2::RING * c2::SLOT);
+#ifdef FI_EXP_LINDMA  // timing experiment: coalesced linear sources (wrong results)
+    for (int i = tid; i < c2::SLOT / 16; i += 512) tab[i] = i < c2::XB / 16 ? 16 * i : (16 * (i - c2::XB / 16) < 10368 ? 16 * (i - c2::XB / 16) : FI_OOB);
+#else
     for (int i = tid; i < c2::SLOT / 16; i += 512) tab[i] = i < c2::XB / 16 ? c2_x_src(i) : c2_dy_src(i - c2::XB / 16);
+#endif
     __syncthreads();
     const int npw = w == 0 ? 11 : (w < 4 ? 10 : 0);  // pieces per wave
     const int nmine = c.nframes > (int)blockIdx.x ? (c.nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
@@ -1077,7 +1108,11 @@ __device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, int nst, W
     const int lane = threadIdx.x & 63, w = wave_id(), tid = threadIdx.x;
     const uint32_t lds0 = lds_addr(smem);
     uint32_t* tab = (uint32_t*)(smem + c3::RING * c3::SLOT);
+#ifdef FI_EXP_LINDMA
+    for (int i = tid; i < (c3::XB + c3::DYB) / 16; i += 512) tab[i] = i < c3::XB / 16 ? (16 * i < 10368 ? 16 * i : FI_OOB) : (16 * (i - c3::XB / 16) < 6272 ? 16 * (i - c3::XB / 16) : FI_OOB);
+#else
     for (int i = tid; i < (c3::XB + c3::DYB) / 16; i += 512) tab[i] = i < c3::XB / 16 ? c3_x_src(i) : c3_dy_src(i - c3::XB / 16);
+#endif
     __syncthreads();
     const int npw = w < 4 ? 11 : 0;
     const int nmine = c.nframes > (int)blockIdx.x ? (c.nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;

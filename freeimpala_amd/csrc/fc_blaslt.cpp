@@ -10,7 +10,9 @@
 //   wgrad    dW[3136][512] = a3^T dh  (fp32 out, straight into the gradient blob)
 // All row-major; hipBLASLt is column-major, so each call computes the transposed product.
 // W is the bf16 copy of the fp32 master in the oracle's [3136][512] order.
-// Algorithms: the heuristic's top candidates are timed once at creation and the fastest kept.
+// Algorithms: the heuristic's top 16 candidates are timed once at creation, on operands filled
+// with hashed bf16 values (the chip's clock under load depends on the data: candidates timed
+// on zero-filled buffers ranked differently from the step), and the fastest kept.
 #include <hip/hip_runtime.h>
 #include <hipblaslt/hipblaslt.h>
 
@@ -18,6 +20,7 @@
 
 #include "fc_blaslt.h"
 #include "fi_common.h"
+#include "kernels.h"
 
 namespace fi {
 
@@ -60,9 +63,9 @@ static int make_gemm(FcBlasLt* F, FcGemm& G, int m, int n, int k, bool ta, bool 
     BLT(hipblasLtMatmulPreferenceCreate(&pref));
     BLT(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &F->wsb,
                                               sizeof(F->wsb)));
-    hipblasLtMatmulHeuristicResult_t res[6];
+    hipblasLtMatmulHeuristicResult_t res[16];
     int got = 0;
-    const int st = (int)hipblasLtMatmulAlgoGetHeuristic(F->h, G.desc, G.la, G.lb, G.ld, G.ld, pref, 6, res, &got);
+    const int st = (int)hipblasLtMatmulAlgoGetHeuristic(F->h, G.desc, G.la, G.lb, G.ld, G.ld, pref, 16, res, &got);
     hipblasLtMatmulPreferenceDestroy(pref);
     if (st != 0 || got == 0) {
         set_error("hipBLASLt: no algorithm for the fc GEMM (m=" + std::to_string(m) + " n=" + std::to_string(n) +
@@ -86,7 +89,7 @@ static int make_gemm(FcBlasLt* F, FcGemm& G, int m, int n, int k, bool ta, bool 
                             F->wsb, s) != 0)
             continue;
         FI_HIP_CHECK(hipEventRecord(e0, s));
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < 3; ++i)
             BLT(hipblasLtMatmul(F->h, G.desc, &alpha, A, G.la, B, G.lb, &beta, D, G.ld, D, G.ld, &res[a].algo,
                                 F->ws, F->wsb, s));
         FI_HIP_CHECK(hipEventRecord(e1, s));
@@ -120,6 +123,11 @@ FcBlasLt* fc_blaslt_create(int rows, const void* a3, const void* w, const void* 
         rc = FI_ERR_OOM;
     }
     constexpr int K = 3136, N = 512;
+    if (rc == FI_OK) {  // timing data (every buffer is overwritten by the step before it is read)
+        rc = fill_hash_bf16((void*)a3, (size_t)rows * K, 1u, s);
+        if (rc == FI_OK) rc = fill_hash_bf16((void*)dh, (size_t)rows * N, 2u, s);
+        if (rc == FI_OK) rc = fill_hash_bf16((void*)w, (size_t)K * N, 3u, s);
+    }
     // column-major views of the row-major products (see the header comment)
     if (rc == FI_OK) rc = make_gemm(F, F->g[0], N, rows, K, false, false, HIP_R_16BF, HIPBLASLT_EPILOGUE_RELU_BIAS, w, a3, h, s);
     if (rc == FI_OK) rc = make_gemm(F, F->g[1], K, rows, N, true, false, HIP_R_16BF, HIPBLASLT_EPILOGUE_DEFAULT, w, dh, da3, s);

@@ -54,6 +54,7 @@ int optimizer_step(int opt, float* p, const float* g, float* m, float* v, size_t
                    float b1, float b2, float eps, double bc1, double bc2, const double* sqnorm,
                    float max_norm, hipStream_t s);
 int to_bf16(const float* src, uint16_t* dst, size_t n, hipStream_t s);
+int fill_hash_bf16(void* dst, size_t n, uint32_t seed, hipStream_t s);
 int synth_launch(uint64_t seed, int T, int B, int B_glob, int b_off, int A, int D, float gamma,
                  float* obs, float* mu, int32_t* act, float* rew, float* disc, uint8_t* frames,
                  hipStream_t s);

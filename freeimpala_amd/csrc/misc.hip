@@ -347,6 +347,28 @@ int to_bf16(const float* src, uint16_t* dst, size_t n, hipStream_t s) {
     return FI_OK;
 }
 
+// bf16 values in [-1, 1) from a 32-bit hash of the index (timing fills: the clock the chip
+// holds depends on the operand data, so candidate algorithms are timed on random-like data)
+__global__ void fill_hash_bf16_kernel(uint16_t* __restrict__ dst, size_t n, uint32_t seed) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x) {
+        uint32_t x = (uint32_t)i * 0x9E3779B9u ^ seed;
+        x ^= x >> 16;
+        x *= 0x85EBCA6Bu;
+        x ^= x >> 13;
+        x *= 0xC2B2AE35u;
+        x ^= x >> 16;
+        const float v = (float)(x >> 8) * (1.0f / 8388608.0f) - 1.0f;
+        dst[i] = __builtin_bit_cast(uint16_t, (__bf16)v);
+    }
+}
+
+int fill_hash_bf16(void* dst, size_t n, uint32_t seed, hipStream_t s) {
+    hipLaunchKernelGGL(fill_hash_bf16_kernel, dim3(grid_for(n)), dim3(256), 0, s, (uint16_t*)dst, n, seed);
+    FI_HIP_CHECK(hipGetLastError());
+    return FI_OK;
+}
+
 }  // namespace fi
 
 extern "C" int fi_synth_trajectories(uint64_t seed, int T, int B, int B_glob, int b_off, int A,

@@ -63,7 +63,17 @@ static double run(hipblasLtHandle_t h, int m, int n, int k, bool ta, bool tb, hi
     return best;
 }
 
-int main() {
+__global__ void fill(uint16_t* d, size_t n, uint32_t seed) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        uint32_t x = (uint32_t)i * 0x9E3779B9u ^ seed;
+        x ^= x >> 16; x *= 0x85EBCA6Bu; x ^= x >> 13; x *= 0xC2B2AE35u; x ^= x >> 16;
+        const float v = (float)(x >> 8) * (1.0f / 8388608.0f) - 1.0f;
+        d[i] = __builtin_bit_cast(uint16_t, (__bf16)v);
+    }
+}
+
+int main(int argc, char** argv) {
+    const bool rnd = argc > 1;
     const long R = 101L * 4096, K = 3136, N = 512;
     void *a3, *w, *h, *dh, *da3, *dw, *ws;
     const size_t wsb = 256 << 20;
@@ -74,9 +84,17 @@ int main() {
     CK(hipMalloc(&w, K * N * 2));
     CK(hipMalloc(&dw, 32 * K * N * 4));
     CK(hipMalloc(&ws, wsb));
-    CK(hipMemset(a3, 0x3c, R * K * 2));
-    CK(hipMemset(dh, 0x3c, R * N * 2));
-    CK(hipMemset(w, 0x3c, K * N * 2));
+    if (rnd) {  // hashed values in [-1, 1)
+        fill<<<2048, 256>>>((uint16_t*)a3, R * K, 1);
+        fill<<<2048, 256>>>((uint16_t*)dh, R * N, 2);
+        fill<<<2048, 256>>>((uint16_t*)w, K * N, 3);
+        CK(hipDeviceSynchronize());
+    } else {
+        CK(hipMemset(a3, 0x3c, R * K * 2));
+        CK(hipMemset(dh, 0x3c, R * N * 2));
+        CK(hipMemset(w, 0x3c, K * N * 2));
+    }
+    std::printf("operands: %s\n", rnd ? "hashed random" : "constant 0x3c3c");
     hipblasLtHandle_t hd;
     CK(hipblasLtCreate(&hd));
     const double fl = 2.0 * R * K * N;
