@@ -43,9 +43,11 @@ def atari_kernel_work(T: int, B: int, A: int) -> dict:
         # conv3 reads a2, da3 (unmasked) and its mask a3, writes da2; conv2 reads a1, da2, writes da1
         "conv2_bwd": (2 * c2, N * (A1 + A2 + A1)),
         "conv3_bwd": (2 * c3, N * (A2 + 2 * A3 + A2)),
+        # fused conv1 + conv2 forward: frames in, a1 and a2 out (a1 is not read back)
+        "conv12_fwd": (c1 + c2, N * (FRAME + A1 + A2)),
     }
 
 
 def atari_step_flops(T: int, B: int, A: int) -> int:
     w = atari_kernel_work(T, B, A)
-    return sum(f for k, (f, _) in w.items() if not k.endswith("_bwd"))
+    return sum(f for k, (f, _) in w.items() if not k.endswith("_bwd") and k != "conv12_fwd")

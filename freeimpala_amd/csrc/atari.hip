@@ -712,6 +712,7 @@ struct AtariImpl {
     std::vector<void*> allocs;
     int cs2 = 0, cs3 = 0;  // class strides for the dgrad GEMMs
     bool fr = true;        // frame-resident kernels (FI_ATARI_GENERIC=1 -> generic GEMMs)
+    bool fuse12 = true;    // conv1+conv2 forward in one kernel (FI_FWD_UNFUSED=1 -> two kernels)
     FcBlasLt* fc = nullptr;  // fc layer GEMMs (hipBLASLt)
 };
 
@@ -721,6 +722,8 @@ int conv2_fwd_fr_launch(const __bf16* a1, const __bf16* w2t, const float* bias, 
                         int grid, hipStream_t s);
 int conv3_fwd_fr_launch(const __bf16* a2, const __bf16* w3t, const float* bias, __bf16* a3, int nframes,
                         int grid, hipStream_t s);
+int conv12_fwd_fr_launch(const uint8_t* frames, const __bf16* w1t, const float* b1, const __bf16* w2t,
+                         const float* b2, __bf16* a1, __bf16* a2, int nframes, int grid, hipStream_t s);
 int conv1_wgrad_fr_launch(const uint8_t* frames, const __bf16* da1, float* slab, float* cs_slab,
                           int nframes, int grid, hipStream_t s);
 int conv2_bwd_fr_launch(const __bf16* a1, const __bf16* da2, const __bf16* w2d, __bf16* da1, float* slab,
@@ -757,6 +760,7 @@ AtariNet* atari_create(int B, int T, int A) {
     I->N = n->N; I->A = A; I->TB = T * B; I->off = Offsets(A);
     const size_t N = n->N;
     I->fr = std::getenv("FI_ATARI_GENERIC") == nullptr;
+    I->fuse12 = std::getenv("FI_FWD_UNFUSED") == nullptr;
     I->cs2 = (int)(((N * 100) + GBM - 1) / GBM * GBM);
     I->cs3 = (int)(((N * 81) + GBM - 1) / GBM * GBM);
     bool ok = dmalloc(I, &I->a1, N * 400 * 32) && dmalloc(I, &I->a2, N * 81 * 64) &&
@@ -821,13 +825,19 @@ int atari_forward(AtariNet* n, const uint8_t* frames, float* logits, float* valu
     const Offsets& o = I->off;
     using namespace geo;
     int rc;
-    if (I->fr) {
+    if (I->fr && I->fuse12) {
+        TagScope ts(tg, "conv12_fwd");
+        rc = conv12_fwd_fr_launch(frames, I->wb.c1T, p + o.c1b, I->wb.c2T, p + o.c2b, I->a1, I->a2, N,
+                                  std::min(N, FR_GRID), s);
+    } else if (I->fr) {
         TagScope ts(tg, "conv1_fwd");
         rc = conv1_fwd_fr_launch(frames, I->wb.c1T, p + o.c1b, I->a1, N, std::min(N, FR_GRID), s);
     } else { TagScope ts(tg, "conv1_fwd"); rc = gemm<256, 32, 4, 1>(Conv1Gather{frames, N * P1}, RowsBf16{I->wb.c1T, C1O, C1K},
                              EpiAct{I->a1, C1O, p + o.c1b, 1.0f / 255.0f}, N * P1, C1O, C1K, s); }
     if (rc) return rc;
-    if (I->fr) {
+    if (I->fr && I->fuse12) {
+        // conv2 ran inside conv12_fwd
+    } else if (I->fr) {
         TagScope ts(tg, "conv2_fwd");
         rc = conv2_fwd_fr_launch(I->a1, I->wb.c2T, p + o.c2b, I->a2, N, std::min(N, FR_GRID), s);
     } else { TagScope ts(tg, "conv2_fwd"); rc = gemm<128, 64, 2, 2>(ConvGather<20, 32, 4, 2, 9>{I->a1, N * P2}, RowsBf16{I->wb.c2T, C2O, C2K},

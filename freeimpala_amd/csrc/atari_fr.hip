@@ -724,6 +724,238 @@ int conv3_fwd_fr_launch(const __bf16* a2, const __bf16* w3t, const float* bias, 
 }
 
 // =====================================================================================
+// Fused conv1 + conv2 forward (frame-resident): a1 is written to HBM once (conv2's backward
+// needs it) but never read back for conv2 -- conv2 takes it from LDS. 8 waves, two per SIMD:
+//   waves 0-3 (conv1 role): conv1 exactly as conv1_fwd_fr (W1 in registers, 16x16x32,
+//     D = [channel][pixel]; pixel tiles w, w+4, ... of the 25); each lane's 16-byte a1
+//     result goes to HBM at once and is HELD in registers until the next iteration writes it
+//     into the conv2 input image (conv_fwd_fr<2>'s chunk-planar class-plane layout);
+//   waves 4-7 (conv2 role): conv2 of the PREVIOUS frame from that image as conv_fwd_fr<2>
+//     (W2 channel half chh in registers, s-grid tiles 3pg..3pg+2), and all raw-frame DMA.
+// Iteration it: [B1] all 8 waves convert raw(it) into the bf16 pair-plane image, the conv1
+// waves also write a1(it-1) into the conv2 image  [B2]  conv1(it) MFMAs on waves 0-3 beside
+// conv2(it-1) MFMAs on waves 4-7 (sharing each SIMD's matrix pipe), raw(it+2) DMA'd into the
+// slot converted in this iteration.
+// LDS: 2 raw slots (57,344) + conv1 image (56,576) + conv2 image (26,880) = 140,800 B.
+// HBM per frame: 28,224 (frame) + 25,600 (a1) + 10,368 (a2) = 64,192 B (vs 89,792 B for the
+// two kernels separately).
+// =====================================================================================
+namespace c12 {
+constexpr int X2 = 1680 * 16;  // conv2 input image (FwdGeo<2>::XB)
+constexpr int LDS = 2 * c1::RAW + c1::IMG + X2;
+}  // namespace c12
+
+// all 512 threads: raw u8 frame (LDS) -> bf16 pair-plane conv1 image
+__device__ __forceinline__ void c12_convert(const char* raw, char* img, int tid) {
+#pragma unroll
+    for (int i = 0; i < (c1::FRAME_LOADS + 511) / 512; ++i) {
+        const int u = tid + 512 * i;
+        if (u < c1::FRAME_LOADS) {
+            bf16x8 lo, hi;
+            u8x16_to_bf16(*(const u32x4*)(raw + 16 * u), lo, hi);
+            *(bf16x8*)(img + 16 * u) = lo;
+            *(bf16x8*)(img + c1::PLANE + 16 * u) = hi;
+        }
+    }
+}
+
+__global__ __launch_bounds__(512, 2) void conv12_fwd_fr(const uint8_t* __restrict__ frames,
+                                                        const __bf16* __restrict__ w1t,  // [32][256]
+                                                        const float* __restrict__ b1,
+                                                        const __bf16* __restrict__ w2t,  // [64][512]
+                                                        const float* __restrict__ b2,
+                                                        __bf16* __restrict__ a1, __bf16* __restrict__ a2,
+                                                        int nframes) {
+    __shared__ __attribute__((aligned(16))) char smem[c12::LDS];
+    char* img = smem + 2 * c1::RAW;
+    char* x2 = img + c1::IMG;
+    const int lane = threadIdx.x & 63, tid = threadIdx.x, w = wave_id();
+    const int g = lane >> 4, c16 = lane & 15, si = c16 ^ ((c16 >> 1) & 4);
+    for (int i = tid; i < c12::X2 / 16; i += 512) ((u32x4*)x2)[i] = u32x4{0, 0, 0, 0};  // gap units
+    const int nmine = nframes > (int)blockIdx.x ? (nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+
+    if (w < 4) {
+        // ---------------- conv1 role
+        bf16x8 bw[2][8];  // lane holds W1[8(i>>2) + 4nt + (i&3), i = lane&15][k = 32ks + 8g..+8]
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int ks = 0; ks < 8; ++ks)
+                bw[nt][ks] = *(const bf16x8*)(w1t + (8 * (c16 >> 2) + 4 * nt + (c16 & 3)) * 256 + 32 * ks + 8 * g);
+        float bch[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bch[j] = b1[8 * g + j];
+        const float inv255 = 1.0f / 255.0f;
+        const int ntile = w == 0 ? 7 : 6;  // tiles w + 4tt < 25
+        u32x4 held[7];                     // a1 of the previous frame, tile tt
+        PH_DECL
+        for (int it = 0; it <= nmine; ++it) {
+            const int f = blockIdx.x + it * gridDim.x;
+            PH(5);
+            lds_barrier();  // B1: raw(it) landed (waited by its issuers); conv1 image and a1 image free
+            PH(1);
+            if (it >= 1) {  // a1(it-1) -> conv2 image (pixel q, chunk g)
+#pragma unroll
+                for (int tt = 0; tt < 7; ++tt)
+                    if (tt < ntile) *(u32x4*)(x2 + 16 * f2_dst(4 * ((w + 4 * tt) * 16 + si) + g)) = held[tt];
+            }
+            if (it < nmine) c12_convert(smem + (it & 1) * c1::RAW, img, tid);
+            PH(2);
+            lds_barrier();  // B2: conv1 image and conv2 image complete
+            PH(1);
+            if (it < nmine) {
+                u32x4* dst = (u32x4*)(a1 + (size_t)f * 12800);
+                auto load = [&](int t, bf16x8* d) {
+                    const int q = t * 16 + si, oy = q / 20, ox = q - 20 * oy;
+                    const char* ab = img + (g & 1) * c1::PLANE + 16 * (oy * 84 + ox + (g >> 1));
+#pragma unroll
+                    for (int ks = 0; ks < 8; ++ks) d[ks] = *(const bf16x8*)(ab + 16 * 21 * ks);
+                };
+                bf16x8 fb[2][8];
+                load(w, fb[0]);
+                __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+                for (int tt = 0; tt < 7; ++tt) {
+                    if (tt < ntile) {
+                        const int t = w + 4 * tt;
+                        if (tt + 1 < ntile) load(t + 4, fb[(tt + 1) & 1]);
+                        const bf16x8* cur = fb[tt & 1];
+                        f32x4 da = f32x4{}, db = f32x4{};
+#pragma unroll
+                        for (int ks = 0; ks < 8; ++ks) {
+                            da = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[0][ks], cur[ks], da, 0, 0, 0);
+                            db = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[1][ks], cur[ks], db, 0, 0, 0);
+                        }
+#pragma unroll
+                        for (int ks = 0; ks < 8; ++ks) {
+                            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                            if (tt + 1 < ntile) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                        }
+                        bf16x8 o;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            o[r] = (__bf16)fmaxf(da[r] * inv255 + bch[r], 0.f);
+                            o[4 + r] = (__bf16)fmaxf(db[r] * inv255 + bch[4 + r], 0.f);
+                        }
+                        held[tt] = __builtin_bit_cast(u32x4, o);
+                        FI_ST16(held[tt], dst + 4 * (t * 16 + si) + g);
+                    }
+                }
+            }
+            PH(3);
+            PH_ITER();
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        PH_FLUSH();
+    } else {
+        // ---------------- conv2 role (+ raw-frame DMA)
+        const int wr = w - 4, chh = wr & 1, pg = wr >> 1;
+        const uint32_t lds0 = lds_addr(smem);
+        bf16x8 wa[2][16];  // lane holds W2[co = 32chh + 8(i>>2) + 4ct + (i&3), i = c16][k = 32ks + 8g..+8]
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+            for (int ks = 0; ks < 16; ++ks)
+                wa[ct][ks] = *(const bf16x8*)(w2t + (size_t)(32 * chh + 8 * (c16 >> 2) + 4 * ct + (c16 & 3)) * 512 +
+                                              32 * ks + 8 * g);
+        float bch[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bch[j] = b2[32 * chh + 8 * g + j];
+        int bbase[3];  // tile i: s = 16 (3pg + i) + sig(c16) on the pitch-10 s-grid, chunk g
+#pragma unroll
+        for (int i = 0; i < 3; ++i) bbase[i] = 16 * (16 * (3 * pg + i) + si + 416 * g + fz(g));
+        auto imm = [](int ks) {  // tap ks = (ky, kx): class plane + position shift
+            const int ky = ks >> 2, kx = ks & 3;
+            return 16 * (10 * (ky >> 1) + (kx >> 1) + 100 * (2 * (ky & 1) + (kx & 1)));
+        };
+        // raw frame k: pieces j = wr + 4i (7 per wave, 28 KiB; bytes past the frame read as 0)
+        auto issue_raw = [&](int k, int slot) {
+            const fi_i32x4 rr = make_rsrc(frames + (size_t)(blockIdx.x + k * gridDim.x) * 28224, 28224);
+#pragma unroll
+            for (int i = 0; i < 7; ++i) {
+                const int j = wr + 4 * i;
+                blds16(rr, 16 * lane + 1024 * j, lds0 + slot * c1::RAW + 1024 * j);
+            }
+            return 7;
+        };
+        // issue order: raw(0) raw(1) | per iteration: raw(it+2), then conv2(it-1)'s 3 stores
+        int issued = 0, m0 = 0, m1 = 0;
+        if (nmine > 0) issued += issue_raw(0, 0);
+        m0 = issued;
+        if (nmine > 1) issued += issue_raw(1, 1);
+        m1 = issued;
+        PH_DECL
+        for (int it = 0; it <= nmine; ++it) {
+            PH(5);
+            if (it < nmine) wait_vmcnt(issued - m0);  // own pieces of raw(it) landed
+            PH(0);
+            lds_barrier();  // B1
+            PH(1);
+            if (it < nmine) c12_convert(smem + (it & 1) * c1::RAW, img, tid);
+            PH(2);
+            lds_barrier();  // B2: raw slot it&1 converted; a1(it-1) in the conv2 image
+            PH(1);
+            int m2 = issued;
+            if (it + 2 < nmine) {
+                issued += issue_raw(it + 2, it & 1);
+                m2 = issued;
+            }
+            PH(4);
+            if (it >= 1) {  // conv2 of frame it-1 from the a1 image
+                const int k = it - 1;
+                u32x4* dst = (u32x4*)(a2 + (size_t)(blockIdx.x + k * gridDim.x) * 5184);
+                constexpr int PD = 4, NSTEP = 3 * 16;
+                bf16x8 fb[PD + 1];
+#pragma unroll
+                for (int st = 0; st < PD; ++st) fb[st] = *(const bf16x8*)(x2 + bbase[st / 16] + imm(st % 16));
+                __builtin_amdgcn_sched_group_barrier(0x100, PD, 0);
+                f32x4 acc0 = f32x4{}, acc1 = f32x4{};
+#pragma unroll
+                for (int st = 0; st < NSTEP; ++st) {
+                    const int i = st / 16, ks = st % 16;
+                    if (st + PD < NSTEP)
+                        fb[(st + PD) % (PD + 1)] = *(const bf16x8*)(x2 + bbase[(st + PD) / 16] + imm((st + PD) % 16));
+                    const bf16x8 b = fb[st % (PD + 1)];
+                    acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[0][ks], b, acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[1][ks], b, acc1, 0, 0, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                    if (st + PD < NSTEP) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    if (ks == 15) {  // tile i done: bias, ReLU, one 16-byte store
+                        const int s = 16 * (3 * pg + i) + si, oy = s / 10, ox = s - 10 * oy;
+                        if (oy < 9 && ox < 9) {
+                            bf16x8 ov;
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                ov[r] = (__bf16)fmaxf(acc0[r] + bch[r], 0.f);
+                                ov[4 + r] = (__bf16)fmaxf(acc1[r] + bch[4 + r], 0.f);
+                            }
+                            FI_ST16(__builtin_bit_cast(u32x4, ov), dst + 8 * (9 * oy + ox) + 4 * chh + g);
+                        }
+                        acc0 = f32x4{};
+                        acc1 = f32x4{};
+                    }
+                }
+                issued += 3;  // every tile has valid pixels: three store instructions
+            }
+            PH(3);
+            PH_ITER();
+            m0 = m1;
+            m1 = m2;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        PH_FLUSH();
+    }
+}
+
+int conv12_fwd_fr_launch(const uint8_t* frames, const __bf16* w1t, const float* b1, const __bf16* w2t,
+                         const float* b2, __bf16* a1, __bf16* a2, int nframes, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(conv12_fwd_fr, dim3(grid), dim3(512), 0, s, frames, w1t, b1, w2t, b2, a1, a2, nframes);
+    FI_HIP_CHECK(hipGetLastError());
+    ph_report("conv12_fwd", grid);
+    return FI_OK;
+}
+
+// =====================================================================================
 // Fused, frame-resident conv backward kernels (dgrad + wgrad + bias of one layer).
 // Per frame, LDS holds the layer input X (= ReLU mask of the data gradient) and the
 // upstream gradient dY; the kernel writes dX = (X > 0) * dgrad(dY, W) once and keeps

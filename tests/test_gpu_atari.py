@@ -154,3 +154,27 @@ def test_frame_resident_kernels_match_generic_path(monkeypatch):
     rel(a["da2"], b["da2"], "da2", l2=1e-3, mx=1e-2)
     rel(a["g"][41056:41056 + 36864], b["g"][41056:41056 + 36864], "c3W", l2=1e-4, mx=1e-3)
     rel(a["g"][77920:77984], b["g"][77920:77984], "c3b", l2=1e-4, mx=1e-3)
+
+
+def test_fused_conv12_forward_matches_separate_kernels(monkeypatch):
+    """conv12_fwd (conv1 + conv2 in one frame-resident kernel, a1 handed over in LDS) computes
+    every output with the same MFMA sequence as conv1_fwd_fr + conv_fwd_fr<2>: a1, a2 and
+    everything downstream must be bit-identical. N = 1,056 frames puts 4-5 frames on every
+    persistent workgroup, so the pipeline's steady state (raw ring, role hand-off) is covered."""
+    T, B = 5, 176
+    outs = {}
+    for mode in ("unfused", "fused"):
+        if mode == "unfused":
+            monkeypatch.setenv("FI_FWD_UNFUSED", "1")
+        else:
+            monkeypatch.delenv("FI_FWD_UNFUSED", raising=False)
+        L = mk(T=T, B=B, seed=5)
+        L.synth(seed=11)
+        L.step_resident()
+        N = (T + 1) * B
+        outs[mode] = {nm: L.tensor(nm, np.uint16, (N, n)) for nm, n in
+                      [("a1", 400 * 32), ("a2", 81 * 64), ("a3", 49 * 64)]}
+        outs[mode]["g"] = L.tensor("grads")
+        L.close()
+    for nm in ("a1", "a2", "a3", "g"):
+        np.testing.assert_array_equal(outs["fused"][nm], outs["unfused"][nm], err_msg=nm)
