@@ -713,6 +713,8 @@ struct AtariImpl {
     int cs2 = 0, cs3 = 0;  // class strides for the dgrad GEMMs
     bool fr = true;        // frame-resident kernels (FI_ATARI_GENERIC=1 -> generic GEMMs)
     bool fuse12 = true;    // conv1+conv2 forward in one kernel (FI_FWD_UNFUSED=1 -> two kernels)
+    bool fuse21 = true;    // conv2 backward + conv1 wgrad in one kernel (FI_BWD_UNFUSED=1 -> two)
+    bool keep_da1 = false; // fused backward also stores da1 to HBM (FI_KEEP_DA1=1; parity checks)
     FcBlasLt* fc = nullptr;  // fc layer GEMMs (hipBLASLt)
 };
 
@@ -726,6 +728,9 @@ int conv12_fwd_fr_launch(const uint8_t* frames, const __bf16* w1t, const float* 
                          const float* b2, __bf16* a1, __bf16* a2, int nframes, int grid, hipStream_t s);
 int conv1_wgrad_fr_launch(const uint8_t* frames, const __bf16* da1, float* slab, float* cs_slab,
                           int nframes, int grid, hipStream_t s);
+int conv21_bwd_fr_launch(const __bf16* a1, const __bf16* da2, const __bf16* w2d, const uint8_t* frames,
+                         __bf16* da1_out, float* slab2, float* cs2, float* slab1, float* cs1, int nframes,
+                         int grid, hipStream_t s);
 int conv2_bwd_fr_launch(const __bf16* a1, const __bf16* da2, const __bf16* w2d, __bf16* da1, float* slab,
                         float* cs_slab, int nframes, int grid, hipStream_t s);
 int conv3_bwd_fr_launch(const __bf16* a2, const __bf16* da3, const __bf16* a3, const __bf16* w3d, __bf16* da2,
@@ -761,6 +766,8 @@ AtariNet* atari_create(int B, int T, int A) {
     const size_t N = n->N;
     I->fr = std::getenv("FI_ATARI_GENERIC") == nullptr;
     I->fuse12 = std::getenv("FI_FWD_UNFUSED") == nullptr;
+    I->fuse21 = std::getenv("FI_BWD_UNFUSED") == nullptr;
+    I->keep_da1 = std::getenv("FI_KEEP_DA1") != nullptr;
     I->cs2 = (int)(((N * 100) + GBM - 1) / GBM * GBM);
     I->cs3 = (int)(((N * 81) + GBM - 1) / GBM * GBM);
     bool ok = dmalloc(I, &I->a1, N * 400 * 32) && dmalloc(I, &I->a2, N * 81 * 64) &&
@@ -902,6 +909,19 @@ int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, con
         FI_A("conv3_dgrad", (gemm<128, 64, 2, 2>(DgradGather<9, 3, 1, 7, 64>{I->da3, N, I->cs3},
                                   ClassRows{I->wb.c3D, 64, C3K, I->cs3, (size_t)64 * C3K, nullptr},
                                   EpiDgrad<9, 1>{I->da2, I->a2, N, I->cs3, 64}, I->cs3, 64, C3K, s)));
+    }
+    // conv2 backward + conv1 wgrad fused: da1 stays in LDS (written to HBM only with FI_KEEP_DA1)
+    if (I->fr && I->fuse21) {
+        const int grid = std::min(N, FR_GRID);
+        float* slab1 = slab + (size_t)grid * C2K * C2O;
+        float* cs1 = cs + (size_t)grid * C2O;
+        FI_A("conv21_bwd", conv21_bwd_fr_launch(I->a1, I->da2, I->wb.c2D, frames, I->keep_da1 ? I->da1 : nullptr,
+                                                slab, cs, slab1, cs1, N, grid, s));
+        FI_A("reduce_slabs", reduce_slabs(slab, grid, (size_t)C2K * C2O, grads + o.c2w, s));
+        FI_A("reduce_slabs", reduce_slabs(cs, grid, (size_t)C2O, grads + o.c2b, s));
+        FI_A("reduce_slabs", reduce_slabs(slab1, grid, (size_t)C1K * C1O, grads + o.c1w, s));
+        FI_A("reduce_slabs", reduce_slabs(cs1, 4 * grid, (size_t)C1O, grads + o.c1b, s));
+        return FI_OK;
     }
     // conv2: wgrad [512][64] + bias, dgrad -> da1 (4 parity classes, masked by a1)
     if (I->fr) {

@@ -1207,7 +1207,11 @@ __global__ __launch_bounds__(512, 2) void conv2_bwd_fr(const __bf16* __restrict_
         const int si = (lane & 15) ^ (((lane & 15) >> 1) & 4);
         const int bd0 = c2::XB + 16 * (si + 128 * g + c2::zc(g));
         const int bd6 = c2::XB + 16 * (min(96 + si, 99) + 128 * g + c2::zc(g));
+#ifdef FI_EXP_NODX  // timing experiment: no dX stores (wrong results)
+        c2_frames(ctx, smem, 0, [&](const char* X, int f) {
+#else
         c2_frames(ctx, smem, 7, [&](const char* X, int f) {
+#endif
             // pixel tile outer: each tile's 16 MFMAs (two accumulator chains; 16x16x32 chains
             // issue back to back) end in its own masked 16-byte store, so the dX stores spread
             // over the frame instead of queueing as a burst. The next tile's 8 fragments are
@@ -1251,7 +1255,13 @@ __global__ __launch_bounds__(512, 2) void conv2_bwd_fr(const __bf16* __restrict_
                         o[r] = m[r] > 0 ? (__bf16)acc0[r] : (__bf16)0.f;
                         o[4 + r] = m[4 + r] > 0 ? (__bf16)acc1[r] : (__bf16)0.f;
                     }
+#if defined(FI_EXP_LINDX)  // timing experiment: same stores, contiguous 1 KiB per instruction
+                    FI_ST16(__builtin_bit_cast(u32x4, o), dst + ((wr * 7 + pt) * 64 + lane) % 1600);
+#elif !defined(FI_EXP_NODX)
                     FI_ST16(__builtin_bit_cast(u32x4, o), dst + 4 * pix + g);
+#else
+                    if (o[0] == (__bf16)1234.f) *(volatile int*)dst = pix;
+#endif
                 }
             }
         });
@@ -1265,6 +1275,393 @@ int conv2_bwd_fr_launch(const __bf16* a1, const __bf16* da2, const __bf16* w2d, 
     FI_HIP_CHECK(hipGetLastError());
     st_report("conv2_bwd");
     ph_report("conv2_bwd", grid);
+    return FI_OK;
+}
+
+// =====================================================================================
+// Fused conv2 backward + conv1 weight gradient (frame-resident): da1 never touches HBM.
+// Per frame, conv2's data gradient da1 = (a1 > 0) * dgrad(da2, W2) is written into an LDS
+// tile [400 pixels][32 channels] (conv1_wgrad_fr's layout with the 16-B chunks of a row
+// XOR-swizzled) and conv1's weight gradient reads it from there. HBM per frame: a1 25,600 + da2 10,368 + raw frame
+// 28,224 = 64,192 B, against 61,568 + 53,824 B for conv2_bwd_fr + conv1_wgrad_fr.
+// 8 waves, two per SIMD, two barriers per frame:
+//   [B1] phase 1: waves 0-3 compute conv2's weight gradient exactly as conv2_bwd_fr (kernel
+//        row ky = w, 128 accumulators), then convert their share of the raw frame (held in
+//        registers, loaded one frame ahead) into the bf16 pair-plane image I; waves 4-7
+//        compute conv2's data gradient (parity class), write the masked da1 into the LDS
+//        tile D, then convert the rest of the raw frame;
+//   [B2] waves 0-3 queue the next frames' a1 / da2 DMA, all waves the next raw frame's
+//        loads; phase 2: conv1's weight gradient on waves 4-7 (kernel rows 2wr, 2wr+1 over
+//        the 25 16-pixel m-steps; both operands by transposed LDS reads).
+// LDS: a1 class-plane image x2 (double-buffered: frame it+2 is DMA'd during frame it),
+// bordered da2 image (single: frame it+1 DMA'd after B2), I, D, the DMA gather table:
+//   2 x 25,600 + 16,384 + 56,576 + 25,600 + 10,496 = 160,256 B.
+// Weight-gradient partials: conv2 [grid][512][64] (+ bias [grid][64]) as conv2_bwd_fr;
+// conv1 [grid][256][32] (x 1/255) as conv1_wgrad_fr; conv1's bias partials come from the
+// data-gradient epilogue, one per parity-class wave: [grid][4][32].
+// =====================================================================================
+namespace c21 {
+constexpr int AXB = c2::XB;                              // 25,600
+constexpr int DYB = c2::DYB;                             // 16,384
+constexpr int O_AX = 0;                                  // 2 slots
+constexpr int O_DY = 2 * AXB;
+constexpr int O_IMG = O_DY + DYB;
+constexpr int O_D = O_IMG + c1::IMG;
+constexpr int O_TAB = O_D + c1::OUT;
+constexpr int LDS = O_TAB + (c2::XB + c2::DYB) / 16 * 4;  // 160,256
+constexpr int NRAW_A = 4;  // 16-B raw-frame units per lane converted by waves 0-3 (units < 1024)
+constexpr int NRAW_B = 3;  // ... by waves 4-7 (units 1024 .. 1763)
+static_assert(256 * (NRAW_A + NRAW_B) >= c1::FRAME_LOADS, "raw-frame split");
+}  // namespace c21
+
+__global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict__ a1,
+                                                        const __bf16* __restrict__ da2,
+                                                        const __bf16* __restrict__ w2d,  // [4][32][256]
+                                                        const uint8_t* __restrict__ frames,
+                                                        __bf16* __restrict__ da1_out,  // optional (parity checks)
+                                                        float* __restrict__ slab2,     // [grid][512][64]
+                                                        float* __restrict__ cs2,       // [grid][64]
+                                                        float* __restrict__ slab1,     // [grid][256][32]
+                                                        float* __restrict__ cs1,       // [grid][4 classes][32]
+                                                        int nframes) {
+    __shared__ __attribute__((aligned(16))) char smem[c21::LDS];
+    const int lane = threadIdx.x & 63, tid = threadIdx.x;
+    const int w = wave_id(), wr = w & 3;
+    const int g = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3, h = lane >> 5, col = lane & 31;
+    const uint32_t lds0 = lds_addr(smem);
+    uint32_t* tab = (uint32_t*)(smem + c21::O_TAB);
+    for (int i = tid; i < (c2::XB + c2::DYB) / 16; i += 512) tab[i] = i < c2::XB / 16 ? c2_x_src(i) : c2_dy_src(i - c2::XB / 16);
+    char* DY = smem + c21::O_DY;
+    char* IMG = smem + c21::O_IMG;
+    char* D = smem + c21::O_D;
+    const int nmine = nframes > (int)blockIdx.x ? (nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+    // The weight-gradient im2col reads of the last m-step run up to ~450 B past the end of an
+    // a1 slot (those rows meet zero dY borders, so they add 0 * value): the bytes there must be
+    // finite. Past slot 1 lies the da2 image; past slot 0 lies slot 1, which is zeroed here when
+    // no frame will ever be DMA'd into it.
+    if (nmine < 2 && tid < 64) ((u32x4*)(smem + c21::O_AX + c21::AXB))[tid] = u32x4{0, 0, 0, 0};
+    __syncthreads();
+    auto frame_of = [&](int k) { return (int)blockIdx.x + k * (int)gridDim.x; };
+
+    // conv1 weight gradient (phase 2, waves 4-7): wave 4 + wr owns k-tiles (kernel rows) 2wr and
+    // 2wr + 1 over the 25 m-steps of 16 pixels; A^T from the frame image and da1 from D, both
+    // by transposed reads, every da1 fragment feeding two MFMAs (four k-tiles per wave over
+    // half the m-steps measured slower: fewer registers left for reading ahead)
+    // da1 tile D: row m (pixel) of 64 B, 16-B chunk c stored at slot c ^ ((m >> 1) & 3) -- the
+    // data-gradient waves' writes (8 lanes on 8 class pixels two apart) then hit 4 slots instead
+    // of one bank group; the transposed reads stay conflict-free and their swizzle is the same
+    // for every m-step (m = 16 ms + m0: bits 1-2 of m come from m0)
+    auto dsw = [](int m, int c) { return 64 * m + 16 * (c ^ ((m >> 1) & 3)); };
+    const int dc = 2 * (g & 1) + (p4 >> 1);
+    const int db0 = dsw(8 * (g >> 1) + q, dc) + 8 * (p4 & 1), db1 = dsw(8 * (g >> 1) + q + 4, dc) + 8 * (p4 & 1);
+    f32x16 acc1[2] = {};
+    auto conv1_wgrad = [&]() {
+        // im2col offset of lane row m = 16ms + m0 (m0 = 8(g>>1) + q + 4hh < 16): output pixel
+        // (oy, ox) = divmod(m, 20), input pixel (4oy + ky, 4ox + kx) with kx = 4(g&1) + p4, so
+        // offset = base + 16 (m + 64 oy); with 16ms = 20a + b (compile time), oy = a + [m0 >= 20 - b]
+        int ua[2], m0a[2];
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            const int m0 = fi_opaque(8 * (g >> 1) + q + 4 * hh);
+            const int kx = 4 * (g & 1) + p4;
+            m0a[hh] = m0;
+            ua[hh] = ((kx >> 1) & 1) * c1::PLANE + 16 * ((2 * wr) * 21 + (kx >> 2)) + 8 * (kx & 1) + 16 * m0;
+        }
+        auto aoff = [&](int ms, int hh) {
+            const int a = 16 * ms / 20, b = 16 * ms - 20 * a;
+            return ua[hh] + 16 * (16 * ms + 64 * a) + (m0a[hh] >= 20 - b ? 1024 : 0);
+        };
+        auto load = [&](int ms, bf16x8* d) {  // [0] da1, [1..2] A of the two k-tiles (m-step ms)
+            d[0] = tr2(D + db0 + 1024 * ms, D + db1 + 1024 * ms);
+            const int o0 = aoff(ms, 0), o1 = aoff(ms, 1);
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt) d[1 + kt] = tr2(IMG + o0 + 336 * kt, IMG + o1 + 336 * kt);
+        };
+        constexpr int PD = 3;  // m-steps read ahead
+        bf16x8 fb[PD + 1][3];
+#pragma unroll
+        for (int ms = 0; ms < PD; ++ms) load(ms, fb[ms]);
+#pragma unroll
+        for (int ms = 0; ms < 25; ++ms) {
+            if (ms + PD < 25) load(ms + PD, fb[(ms + PD) % (PD + 1)]);
+            const bf16x8* cur = fb[ms % (PD + 1)];
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt)
+                acc1[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[1 + kt], cur[0], acc1[kt], 0, 0, 0);
+        }
+    };
+
+    if (w < 4) {
+        // ---------------- conv2 weight gradient (as conv2_bwd_fr), raw-frame conversion,
+        // all a1 / da2 DMA
+        auto issue_ax = [&](int k, int slot) {  // pieces j = w + 4i < 25 of frame k's a1 image
+            const fi_i32x4 xr = make_rsrc(a1 + (size_t)frame_of(k) * 12800, 25600);
+            const uint32_t base = lds0 + c21::O_AX + slot * c21::AXB;
+            uint32_t o[7];
+#pragma unroll
+            for (int i = 0; i < 7; ++i) o[i] = tab[64 * min(w + 4 * i, c2::NX - 1) + lane];
+            int n = 0;
+#pragma unroll
+            for (int i = 0; i < 7; ++i) {
+                const int j = w + 4 * i;
+                if (j < c2::NX) {
+                    blds16(xr, o[i], base + 1024 * j);
+                    ++n;
+                }
+            }
+            return n;
+        };
+        auto issue_dy = [&](int k) {  // pieces w + 4i of frame k's bordered da2 image
+            const fi_i32x4 dr = make_rsrc(da2 + (size_t)frame_of(k) * 5184, 10368);
+            uint32_t o[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) o[i] = tab[64 * (c2::NX + w + 4 * i) + lane];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) blds16(dr, o[i], lds0 + c21::O_DY + 1024 * (w + 4 * i));
+            return 4;
+        };
+        // raw frame units tid + 256i (< 256 NRAW_A) in registers, loaded one frame ahead (plain loads:
+        // the compiler's own vmcnt waits cover them; they are issued after this wave's DMA)
+        u32x4 rr[c21::NRAW_A];
+        auto load_raw = [&](int k) {
+            const u32x4* src = (const u32x4*)(frames + (size_t)frame_of(k) * 28224);
+#pragma unroll
+            for (int i = 0; i < c21::NRAW_A; ++i) rr[i] = src[tid + 256 * i];
+        };
+        const int mu0 = 8 * (g >> 1) + q, c = 2 * (g & 1) + (p4 >> 1);
+        const int ba0 = 64 * (200 * (wr & 1) + mu0 + 10 * (wr >> 1)) + 2 * (16 * (g & 1) + 4 * p4);
+        const int bb0 = 16 * (11 + mu0 + 128 * c + c2::zc(c)) + 8 * (p4 & 1);
+        f32x16 accw[4][2];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) { accw[t][0] = f32x16{}; accw[t][1] = f32x16{}; }
+        float bsum0 = 0.f, bsum1_ = 0.f;
+        int issued = 0, m_dy = 0;
+        if (nmine > 0) issued += issue_ax(0, 0);
+        if (nmine > 1) issued += issue_ax(1, 1);
+        if (nmine > 0) issued += issue_dy(0);
+        m_dy = issued;
+        if (nmine > 0) {
+            load_raw(0);
+            issued += c21::NRAW_A;
+        }
+        PH_DECL
+        for (int it = 0; it < nmine; ++it) {
+            PH(5);
+            wait_vmcnt(issued - m_dy);  // own pieces of da2(it) landed (a1(it) is older)
+            PH(0);
+            lds_barrier();  // B1: frame it's images in LDS; frame it-1's D and image consumed
+            PH(1);
+            {
+                const char* XA = smem + c21::O_AX + (it & 1) * c21::AXB + ba0;
+                const char* XB_ = DY + bb0;
+                bf16x8 fb[2][6];  // [0] b0, [1] b1, [2..5] A of kx = 0..3
+                auto load = [&](int ms, bf16x8* d) {
+                    const int ob = 16 * 16 * ms, oa = 64 * 16 * ms;
+                    d[0] = tr2(XB_ + ob, XB_ + ob + 64);
+                    d[1] = tr2(XB_ + ob + 8192, XB_ + ob + 64 + 8192);  // chunk + 4
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        const int ao = oa + 6400 * (t & 1) + 64 * (t >> 1);
+                        d[2 + t] = tr2(XA + ao, XA + ao + 256);
+                    }
+                };
+                load(0, fb[0]);
+                __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+#pragma unroll
+                for (int ms = 0; ms < 6; ++ms) {
+                    const bf16x8* cur = fb[ms & 1];
+                    if (ms + 1 < 6) load(ms + 1, fb[(ms + 1) & 1]);
+                    float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) { s0 += (float)cur[0][j]; s1 += (float)cur[1][j]; }
+                    bsum0 += s0;
+                    bsum1_ += s1;
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        accw[t][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[2 + t], cur[0], accw[t][0], 0, 0, 0);
+                        accw[t][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[2 + t], cur[1], accw[t][1], 0, 0, 0);
+                    }
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                        if (ms + 1 < 6) {
+                            if (k < 4) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                            else __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                        }
+                    }
+                }
+            }
+            PH(2);
+#pragma unroll
+            for (int i = 0; i < c21::NRAW_A; ++i) {  // raw(it) -> bf16 pair-plane image (free since B1)
+                const int u = tid + 256 * i;
+                bf16x8 lo, hi;
+                u8x16_to_bf16(rr[i], lo, hi);
+                *(bf16x8*)(IMG + 16 * u) = lo;
+                *(bf16x8*)(IMG + c1::PLANE + 16 * u) = hi;
+            }
+            PH(3);
+            lds_barrier();  // B2: D and the image complete; da2 image and a1 slot it&1 consumed
+            PH(1);
+            if (it + 1 < nmine) {
+                issued += issue_dy(it + 1);
+                m_dy = issued;
+            }
+            if (it + 2 < nmine) issued += issue_ax(it + 2, it & 1);
+            if (it + 1 < nmine) {
+                load_raw(it + 1);
+                issued += c21::NRAW_A;
+            }
+            PH(4);
+            PH_ITER();
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        PH_FLUSH();
+        float* out = slab2 + (size_t)blockIdx.x * 512 * 64;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int k = 128 * wr + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    out[k * 64 + 32 * ct + col] = accw[t][ct][r];
+                }
+        if (wr == 0) {
+            const float o0 = __shfl_xor(bsum0, 32, 64), o1 = __shfl_xor(bsum1_, 32, 64);
+            if (lane < 32) {
+                cs2[(size_t)blockIdx.x * 64 + lane] = bsum0 + o0;
+                cs2[(size_t)blockIdx.x * 64 + 32 + lane] = bsum1_ + o1;
+            }
+        }
+    } else {
+        // ---------------- conv2 data gradient -> D
+        const int ty = wr >> 1, tx = wr & 1;
+        bf16x8 bw[2][8];  // W2 class slice (conv2_bwd_fr)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int ks = 0; ks < 8; ++ks) {
+                const int i = lane & 15, ci = 8 * (i >> 2) + 4 * nt + (i & 3);
+                bw[nt][ks] = *(const bf16x8*)(w2d + ((size_t)(wr * 32 + ci)) * 256 + 32 * ks + 8 * g);
+            }
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the weights are in before the frame loop
+        const int t4 = tid - 256;
+        u32x4 rr[c21::NRAW_B];  // raw frame units 256 NRAW_A + t4 + 256i, loaded one frame ahead
+        auto load_raw = [&](int k) {
+            const u32x4* src = (const u32x4*)(frames + (size_t)frame_of(k) * 28224);
+#pragma unroll
+            for (int i = 0; i < c21::NRAW_B; ++i) {
+                const int u = 256 * c21::NRAW_A + t4 + 256 * i;
+                rr[i] = u < c1::FRAME_LOADS ? src[u] : u32x4{0, 0, 0, 0};
+            }
+        };
+        if (nmine > 0) load_raw(0);
+        const int si = (lane & 15) ^ (((lane & 15) >> 1) & 4);
+        const int bd0 = 16 * (si + 128 * g + c2::zc(g));
+        const int bd6 = 16 * (min(96 + si, 99) + 128 * g + c2::zc(g));
+        float bs8[8] = {};  // conv1 bias partials: channels 8g + j of this lane's da1 pixels
+        PH_DECL
+        for (int it = 0; it < nmine; ++it) {
+            const int f = frame_of(it);
+            PH(5);
+            lds_barrier();  // B1
+            PH(1);
+            {  // conv2 data gradient of class (ty, tx) -> D (and da1_out)
+                const char* X = smem + c21::O_AX + (it & 1) * c21::AXB;
+                u32x4* dst = da1_out ? (u32x4*)(da1_out + (size_t)f * 12800) : nullptr;
+                // step st = (pixel tile pt, k-step ks): dY fragment read PD steps ahead
+                auto frag = [&](int st) {
+                    const int pt = st >> 3, ks = st & 7, tap = ks >> 1, kty = tap >> 1, ktx = tap & 1;
+                    return *(const bf16x8*)(DY + (pt < 6 ? bd0 + 256 * pt : bd6) + 16 * (11 - 10 * kty - ktx) +
+                                            8192 * (ks & 1));
+                };
+                constexpr int PD = 4, NSTEP = 7 * 8;
+                bf16x8 fb[PD + 1];
+#pragma unroll
+                for (int st = 0; st < PD; ++st) fb[st] = frag(st);
+                __builtin_amdgcn_sched_group_barrier(0x100, PD, 0);
+                f32x4 ac0 = f32x4{}, ac1 = f32x4{};
+#pragma unroll
+                for (int st = 0; st < NSTEP; ++st) {
+                    const int pt = st >> 3, ks = st & 7;
+                    if (st + PD < NSTEP) fb[(st + PD) % (PD + 1)] = frag(st + PD);
+                    const bf16x8 b = fb[st % (PD + 1)];
+                    ac0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[0][ks], b, ac0, 0, 0, 0);
+                    ac1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[1][ks], b, ac1, 0, 0, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                    if (st + PD < NSTEP) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    if (ks == 7) {  // tile pt done: mask by (a1 > 0), into D
+                        const int ri = pt * 16 + si;
+                        if (pt < 6 || ri < 100) {
+                            const int iyq = ri / 10, ixq = ri - 10 * iyq;
+                            const int pix = (2 * iyq + ty) * 20 + 2 * ixq + tx;
+                            const s16x8 m = *(const s16x8*)(X + 64 * (100 * wr + ri) + 16 * g);
+                            bf16x8 o;
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                o[r] = m[r] > 0 ? (__bf16)ac0[r] : (__bf16)0.f;
+                                o[4 + r] = m[4 + r] > 0 ? (__bf16)ac1[r] : (__bf16)0.f;
+                            }
+                            const u32x4 ov = __builtin_bit_cast(u32x4, o);
+                            *(u32x4*)(D + dsw(pix, g)) = ov;
+#pragma unroll
+                            for (int j = 0; j < 8; ++j) bs8[j] += (float)o[j];
+                            if (dst) FI_ST16(ov, dst + 4 * pix + g);
+                        }
+                        ac0 = f32x4{};
+                        ac1 = f32x4{};
+                    }
+                }
+            }
+            PH(2);
+#pragma unroll
+            for (int i = 0; i < c21::NRAW_B; ++i) {  // raw(it), the last units -> image
+                const int u = 256 * c21::NRAW_A + t4 + 256 * i;
+                if (u < c1::FRAME_LOADS) {
+                    bf16x8 lo, hi;
+                    u8x16_to_bf16(rr[i], lo, hi);
+                    *(bf16x8*)(IMG + 16 * u) = lo;
+                    *(bf16x8*)(IMG + c1::PLANE + 16 * u) = hi;
+                }
+            }
+            PH(4);
+            lds_barrier();  // B2: D and the image complete
+            PH(1);
+            if (it + 1 < nmine) load_raw(it + 1);
+            conv1_wgrad();
+            PH(3);
+            PH_ITER();
+        }
+        PH_FLUSH();
+        // conv1 bias partial of this class wave: sum over the 16 lanes of each channel group
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) bs8[j] += __shfl_xor(bs8[j], o, 64);
+        if ((lane & 15) == 0) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) cs1[((size_t)blockIdx.x * 4 + wr) * 32 + 8 * g + j] = bs8[j];
+        }
+    }
+    if (w >= 4) {  // conv1 weight-gradient slab rows k = 32(2wr + kt) + (r&3) + 8(r>>2) + 4(lane>>5)
+        const float inv255 = 1.0f / 255.0f;
+        float* out1 = slab1 + (size_t)blockIdx.x * 256 * 32;
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                out1[(32 * (2 * wr + kt) + (r & 3) + 8 * (r >> 2) + 4 * h) * 32 + col] = acc1[kt][r] * inv255;
+    }
+}
+
+int conv21_bwd_fr_launch(const __bf16* a1, const __bf16* da2, const __bf16* w2d, const uint8_t* frames,
+                         __bf16* da1_out, float* slab2, float* cs2, float* slab1, float* cs1, int nframes,
+                         int grid, hipStream_t s) {
+    hipLaunchKernelGGL(conv21_bwd_fr, dim3(grid), dim3(512), 0, s, a1, da2, w2d, frames, da1_out, slab2, cs2,
+                       slab1, cs1, nframes);
+    FI_HIP_CHECK(hipGetLastError());
+    ph_report("conv21_bwd", grid);
     return FI_OK;
 }
 
@@ -1504,7 +1901,11 @@ __global__ __launch_bounds__(512, 2) void conv3_bwd_fr(const __bf16* __restrict_
         const int cg = g;  // dY chunk of k-step ks: g + 4(ks&1)
         const int bdA = c3::XB + 16 * (48 * ph + si + 128 * cg + c3::zc(cg));
         const int bdC = c3::XB + 16 * (min(48 * ph + 32 + si, 80) + 128 * cg + c3::zc(cg));
+#ifdef FI_EXP_NODX
+        c3_frames(ctx, smem, 0, [&](const char* X, int f) {
+#else
         c3_frames(ctx, smem, 3, [&](const char* X, int f) {
+#endif
             f32x4 acc[3][2];
 #pragma unroll
             for (int ti = 0; ti < 3; ++ti) { acc[ti][0] = f32x4{}; acc[ti][1] = f32x4{}; }
@@ -1548,7 +1949,13 @@ __global__ __launch_bounds__(512, 2) void conv3_bwd_fr(const __bf16* __restrict_
                         o[r] = m[r] > 0 ? (__bf16)acc[ti][0][r] : (__bf16)0.f;
                         o[4 + r] = m[4 + r] > 0 ? (__bf16)acc[ti][1][r] : (__bf16)0.f;
                     }
+#if defined(FI_EXP_LINDX)
+                    FI_ST16(__builtin_bit_cast(u32x4, o), dst + ((wr * 3 + ti) * 64 + lane) % 648);
+#elif !defined(FI_EXP_NODX)
                     FI_ST16(__builtin_bit_cast(u32x4, o), dst + 8 * ri + c);
+#else
+                    if (o[0] == (__bf16)1234.f) *(volatile int*)dst = ri;
+#endif
                 }
             }
         });

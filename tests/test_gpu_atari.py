@@ -42,8 +42,9 @@ def test_atari_synth_frames_bit_exact(orc):
 
 
 @pytest.mark.parametrize("T,B", [(2, 16), (3, 32)])
-def test_atari_forward_backward_parity(orc, T, B):
+def test_atari_forward_backward_parity(orc, T, B, monkeypatch):
     A = 18
+    monkeypatch.setenv("FI_KEEP_DA1", "1")  # the fused conv2/conv1 backward keeps da1 in LDS otherwise
     L = mk(T=T, B=B, A=A)
     L.synth(seed=T * 100 + B)
     N = (T + 1) * B
@@ -130,6 +131,7 @@ def test_frame_resident_kernels_match_generic_path(monkeypatch):
     layer (different fp32 summation order): activations within one bf16 ulp, grads 1e-4."""
     T, B = 2, 16
     outs = {}
+    monkeypatch.setenv("FI_KEEP_DA1", "1")
     for mode in ("generic", "fr"):
         if mode == "generic":
             monkeypatch.setenv("FI_ATARI_GENERIC", "1")
@@ -178,3 +180,48 @@ def test_fused_conv12_forward_matches_separate_kernels(monkeypatch):
         L.close()
     for nm in ("a1", "a2", "a3", "g"):
         np.testing.assert_array_equal(outs["fused"][nm], outs["unfused"][nm], err_msg=nm)
+
+
+def test_fused_conv21_backward_matches_separate_kernels(monkeypatch):
+    """conv21_bwd (conv2 backward + conv1 weight gradient in one kernel, da1 handed over in LDS)
+    against conv2_bwd_fr + conv1_wgrad_fr: da1 (stored on request) and the conv2 gradients are
+    bit-identical (same MFMA sequences and frame order); the conv1 weight gradient sums the
+    same products in another order (fp32 rounding only). 4-5 frames per workgroup."""
+    T, B = 5, 176
+    outs = {}
+    for mode in ("unfused", "fused"):
+        if mode == "unfused":
+            monkeypatch.setenv("FI_BWD_UNFUSED", "1")
+        else:
+            monkeypatch.delenv("FI_BWD_UNFUSED", raising=False)
+        monkeypatch.setenv("FI_KEEP_DA1", "1")
+        L = mk(T=T, B=B, seed=5)
+        L.synth(seed=13)
+        L.step_resident()
+        N = (T + 1) * B
+        outs[mode] = dict(da1=L.tensor("da1", np.uint16, (N, 400 * 32)), g=L.tensor("grads"))
+        L.close()
+    u, f = outs["unfused"], outs["fused"]
+    np.testing.assert_array_equal(f["da1"], u["da1"], err_msg="da1")
+    np.testing.assert_array_equal(f["g"][8224:], u["g"][8224:], err_msg="conv2 and later gradients")
+    rel(f["g"][:8192], u["g"][:8192], "c1W", l2=1e-5, mx=1e-4)
+    rel(f["g"][8192:8224], u["g"][8192:8224], "c1b", l2=1e-5, mx=1e-4)
+
+
+def test_fused_conv21_backward_without_da1_store(monkeypatch):
+    """The production path (da1 never written to HBM) gives the same gradients as with the
+    optional da1 store."""
+    T, B = 3, 96
+    gs = []
+    for keep in ("1", None):
+        if keep:
+            monkeypatch.setenv("FI_KEEP_DA1", keep)
+        else:
+            monkeypatch.delenv("FI_KEEP_DA1", raising=False)
+        monkeypatch.delenv("FI_BWD_UNFUSED", raising=False)
+        L = mk(T=T, B=B, seed=2)
+        L.synth(seed=21)
+        L.step_resident()
+        gs.append(L.tensor("grads"))
+        L.close()
+    np.testing.assert_array_equal(gs[0], gs[1])
