@@ -1286,10 +1286,11 @@ int conv2_bwd_fr_launch(const __bf16* a1, const __bf16* da2, const __bf16* w2d, 
 // 28,224 = 64,192 B, against 61,568 + 53,824 B for conv2_bwd_fr + conv1_wgrad_fr.
 // 8 waves, two per SIMD, two barriers per frame:
 //   [B1] phase 1: waves 0-3 compute conv2's weight gradient exactly as conv2_bwd_fr (kernel
-//        row ky = w, 128 accumulators), then convert their share of the raw frame (held in
-//        registers, loaded one frame ahead) into the bf16 pair-plane image I; waves 4-7
-//        compute conv2's data gradient (parity class), write the masked da1 into the LDS
-//        tile D, then convert the rest of the raw frame;
+//        row ky = w, 128 accumulators), then convert the raw frame (held in their registers,
+//        loaded one frame ahead; FI_C21_NRAW_A < 7 moves a share to waves 4-7, measured
+//        slower: their loads in flight stall phase 2) into the bf16 pair-plane image I;
+//        waves 4-7 compute conv2's data gradient (parity class) and write the masked da1
+//        into the LDS tile D;
 //   [B2] waves 0-3 queue the next frames' a1 / da2 DMA, all waves the next raw frame's
 //        loads; phase 2: conv1's weight gradient on waves 4-7 (kernel rows 2wr, 2wr+1 over
 //        the 25 16-pixel m-steps; both operands by transposed LDS reads).
@@ -1309,8 +1310,11 @@ constexpr int O_IMG = O_DY + DYB;
 constexpr int O_D = O_IMG + c1::IMG;
 constexpr int O_TAB = O_D + c1::OUT;
 constexpr int LDS = O_TAB + (c2::XB + c2::DYB) / 16 * 4;  // 160,256
-constexpr int NRAW_A = 4;  // 16-B raw-frame units per lane converted by waves 0-3 (units < 1024)
-constexpr int NRAW_B = 3;  // ... by waves 4-7 (units 1024 .. 1763)
+#ifndef FI_C21_NRAW_A
+#define FI_C21_NRAW_A 7
+#endif
+constexpr int NRAW_A = FI_C21_NRAW_A;  // 16-B raw-frame units per lane converted by waves 0-3
+constexpr int NRAW_B = 7 - NRAW_A;     // ... by waves 4-7 (the rest of the 1,764)
 static_assert(256 * (NRAW_A + NRAW_B) >= c1::FRAME_LOADS, "raw-frame split");
 }  // namespace c21
 
@@ -1426,7 +1430,10 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
         auto load_raw = [&](int k) {
             const u32x4* src = (const u32x4*)(frames + (size_t)frame_of(k) * 28224);
 #pragma unroll
-            for (int i = 0; i < c21::NRAW_A; ++i) rr[i] = src[tid + 256 * i];
+            for (int i = 0; i < c21::NRAW_A; ++i) {
+                const int u = tid + 256 * i;
+                rr[i] = (256 * (i + 1) <= c1::FRAME_LOADS || u < c1::FRAME_LOADS) ? src[u] : u32x4{0, 0, 0, 0};
+            }
         };
         const int mu0 = 8 * (g >> 1) + q, c = 2 * (g & 1) + (p4 >> 1);
         const int ba0 = 64 * (200 * (wr & 1) + mu0 + 10 * (wr >> 1)) + 2 * (16 * (g & 1) + 4 * p4);
@@ -1495,10 +1502,12 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
 #pragma unroll
             for (int i = 0; i < c21::NRAW_A; ++i) {  // raw(it) -> bf16 pair-plane image (free since B1)
                 const int u = tid + 256 * i;
-                bf16x8 lo, hi;
-                u8x16_to_bf16(rr[i], lo, hi);
-                *(bf16x8*)(IMG + 16 * u) = lo;
-                *(bf16x8*)(IMG + c1::PLANE + 16 * u) = hi;
+                if (256 * (i + 1) <= c1::FRAME_LOADS || u < c1::FRAME_LOADS) {
+                    bf16x8 lo, hi;
+                    u8x16_to_bf16(rr[i], lo, hi);
+                    *(bf16x8*)(IMG + 16 * u) = lo;
+                    *(bf16x8*)(IMG + c1::PLANE + 16 * u) = hi;
+                }
             }
             PH(3);
             lds_barrier();  // B2: D and the image complete; da2 image and a1 slot it&1 consumed
@@ -1547,7 +1556,7 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
             }
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the weights are in before the frame loop
         const int t4 = tid - 256;
-        u32x4 rr[c21::NRAW_B];  // raw frame units 256 NRAW_A + t4 + 256i, loaded one frame ahead
+        u32x4 rr[c21::NRAW_B > 0 ? c21::NRAW_B : 1];  // raw units 256 NRAW_A + t4 + 256i, one frame ahead
         auto load_raw = [&](int k) {
             const u32x4* src = (const u32x4*)(frames + (size_t)frame_of(k) * 28224);
 #pragma unroll
@@ -1576,11 +1585,17 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                     return *(const bf16x8*)(DY + (pt < 6 ? bd0 + 256 * pt : bd6) + 16 * (11 - 10 * kty - ktx) +
                                             8192 * (ks & 1));
                 };
-                constexpr int PD = 4, NSTEP = 7 * 8;
+                constexpr int PD = 6, NSTEP = 7 * 8;
                 bf16x8 fb[PD + 1];
 #pragma unroll
                 for (int st = 0; st < PD; ++st) fb[st] = frag(st);
                 __builtin_amdgcn_sched_group_barrier(0x100, PD, 0);
+                // the (a1 > 0) mask of a tile is read when the tile starts, a tile's MFMAs
+                // before its epilogue needs it
+                auto mask_of = [&](int pt) {
+                    return *(const s16x8*)(X + 64 * (100 * wr + min(pt * 16 + si, 99)) + 16 * g);
+                };
+                s16x8 mk = mask_of(0);
                 f32x4 ac0 = f32x4{}, ac1 = f32x4{};
 #pragma unroll
                 for (int st = 0; st < NSTEP; ++st) {
@@ -1592,11 +1607,12 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                     __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
                     if (st + PD < NSTEP) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                     if (ks == 7) {  // tile pt done: mask by (a1 > 0), into D
+                        const s16x8 m = mk;
+                        if (pt + 1 < 7) mk = mask_of(pt + 1);
                         const int ri = pt * 16 + si;
                         if (pt < 6 || ri < 100) {
                             const int iyq = ri / 10, ixq = ri - 10 * iyq;
                             const int pix = (2 * iyq + ty) * 20 + 2 * ixq + tx;
-                            const s16x8 m = *(const s16x8*)(X + 64 * (100 * wr + ri) + 16 * g);
                             bf16x8 o;
 #pragma unroll
                             for (int r = 0; r < 4; ++r) {
@@ -1604,7 +1620,9 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                                 o[4 + r] = m[4 + r] > 0 ? (__bf16)ac1[r] : (__bf16)0.f;
                             }
                             const u32x4 ov = __builtin_bit_cast(u32x4, o);
+#ifndef FI_EXP_NODW  // timing experiment: no da1 tile writes (wrong results)
                             *(u32x4*)(D + dsw(pix, g)) = ov;
+#endif
 #pragma unroll
                             for (int j = 0; j < 8; ++j) bs8[j] += (float)o[j];
                             if (dst) FI_ST16(ov, dst + 4 * pix + g);
