@@ -45,9 +45,11 @@ def atari_kernel_work(T: int, B: int, A: int) -> dict:
         "conv3_bwd": (2 * c3, N * (A2 + 2 * A3 + A2)),
         # fused conv1 + conv2 forward: frames in, a1 and a2 out (a1 is not read back)
         "conv12_fwd": (c1 + c2, N * (FRAME + A1 + A2)),
+        # fused conv2 backward + conv1 weight gradient: a1, da2, frames in (da1 stays in LDS)
+        "conv21_bwd": (2 * c2 + c1, N * (A1 + A2 + FRAME)),
     }
 
 
 def atari_step_flops(T: int, B: int, A: int) -> int:
     w = atari_kernel_work(T, B, A)
-    return sum(f for k, (f, _) in w.items() if not k.endswith("_bwd") and k != "conv12_fwd")
+    return sum(f for k, (f, _) in w.items() if not k.endswith("_bwd") and k != "conv12_fwd")  # each layer once

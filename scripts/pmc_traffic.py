@@ -25,6 +25,8 @@ TAGS = {
     "conv1_wgrad": "conv1_wgrad_fr",
     "conv2_fwd": "conv_fwd_fr<2>",
     "conv3_fwd": "conv_fwd_fr<3>",
+    "conv12_fwd": "conv12_fwd_fr",
+    "conv21_bwd": "conv21_bwd_fr",
 }
 
 
