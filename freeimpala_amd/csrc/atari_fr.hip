@@ -1904,8 +1904,8 @@ __global__ __launch_bounds__(512, 2) void conv3_bwd_fr(const __bf16* __restrict_
     } else {
         // data gradient: channel half chh = wr&1 (tiles ct = 0, 1 of 16 channels; row i of tile
         // ct is channel 32chh + 8(i>>2) + 4ct + (i&3), so lane group g ends with channels
-        // 32chh + 8g..+8 of its pixel), pixel tiles 3ph..3ph+2 (ph = wr>>1), lane i of tile pt
-        // on pixel 16pt + sig(i)
+        // 32chh + 8g..+8 of its pixel), three pixel tiles per wave ({1, 2, 5} for ph = wr>>1 = 0,
+        // {0, 3, 4} for ph = 1), lane i of tile pt on pixel 16pt + sig(i)
         const int chh = wr & 1, ph = wr >> 1;
         s16x8 bw[2][18];  // lane holds W[ci(ct, lane&15)][k = 32ks + 8g..+8]
 #pragma unroll
@@ -1917,48 +1917,55 @@ __global__ __launch_bounds__(512, 2) void conv3_bwd_fr(const __bf16* __restrict_
             }
         const int si = (lane & 15) ^ (((lane & 15) >> 1) & 4);
         const int cg = g;  // dY chunk of k-step ks: g + 4(ks&1)
-        const int bdA = c3::XB + 16 * (48 * ph + si + 128 * cg + c3::zc(cg));
-        const int bdC = c3::XB + 16 * (min(48 * ph + 32 + si, 80) + 128 * cg + c3::zc(cg));
-#ifdef FI_EXP_NODX
-        c3_frames(ctx, smem, 0, [&](const char* X, int f) {
-#else
-        c3_frames(ctx, smem, 3, [&](const char* X, int f) {
-#endif
+        // Tap skipping: dX pixel (iy, ix) meets dY row iy - ky, which exists only for
+        // 0 <= iy - ky <= 6 (the zero border supplies the rest). Pixel tiles are 16 pixels of
+        // the 9-wide image, so tile 0 (rows 0-1) never needs kernel row 2, tile 4 (rows 7-8)
+        // never row 0 and tile 5 (pixel 80) only row 2: their all-zero k-steps are skipped
+        // (the sums are unchanged bit for bit). Tiles {1, 2, 5} and {0, 3, 4} then carry 42
+        // k-step x tile units each (84 MFMAs per wave instead of 108).
+        auto work = [&](auto phc, const char* X, int f) {
+            constexpr int PH = decltype(phc)::value;
+            constexpr auto tile = [](int ti) { return PH == 0 ? (ti == 0 ? 1 : ti == 1 ? 2 : 5) : (ti == 0 ? 0 : ti == 1 ? 3 : 4); };
+            constexpr auto active = [](int ks, int pt) {
+                const int lo = pt == 4 ? 6 : (pt == 5 ? 12 : 0), hi = pt == 0 ? 12 : 18;
+                return ks >= lo && ks < hi;
+            };
+            int bd[3];
+#pragma unroll
+            for (int ti = 0; ti < 3; ++ti) bd[ti] = c3::XB + 16 * (min(16 * tile(ti) + si, 80) + 128 * cg + c3::zc(cg));
             f32x4 acc[3][2];
 #pragma unroll
             for (int ti = 0; ti < 3; ++ti) { acc[ti][0] = f32x4{}; acc[ti][1] = f32x4{}; }
-            bf16x8 fb[2][3];
+            constexpr int PD = 3;  // k-steps of fragments read ahead
+            bf16x8 fb[PD + 1][3];
             auto load = [&](int ks, bf16x8* d) {  // k = 64 tap + co: tap = ks>>1, co half = ks&1 (chunk + 4)
                 const int tap = ks >> 1, ky = tap / 3, kx = tap - 3 * ky;
                 const int off = 16 * (20 - 9 * ky - kx) + 8192 * (ks & 1);
-                d[0] = *(const bf16x8*)(X + bdA + off);
-                d[1] = *(const bf16x8*)(X + bdA + 256 + off);
-                d[2] = *(const bf16x8*)(X + bdC + off);
+#pragma unroll
+                for (int ti = 0; ti < 3; ++ti)
+                    if (active(ks, tile(ti))) d[ti] = *(const bf16x8*)(X + bd[ti] + off);
             };
-            load(0, fb[0]);
-            __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+#pragma unroll
+            for (int ks = 0; ks < PD; ++ks) load(ks, fb[ks]);
 #pragma unroll
             for (int ks = 0; ks < 18; ++ks) {
-                const bf16x8* cur = fb[ks & 1];
-                if (ks + 1 < 18) load(ks + 1, fb[(ks + 1) & 1]);
+                const bf16x8* cur = fb[ks % (PD + 1)];
+                if (ks + PD < 18) load(ks + PD, fb[(ks + PD) % (PD + 1)]);
 #pragma unroll
                 for (int ti = 0; ti < 3; ++ti) {
-                    acc[ti][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bw[0][ks]), cur[ti],
-                                                                        acc[ti][0], 0, 0, 0);
-                    acc[ti][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bw[1][ks]), cur[ti],
-                                                                        acc[ti][1], 0, 0, 0);
-                }
-#pragma unroll
-                for (int ti = 0; ti < 3; ++ti) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-                    if (ks + 1 < 18) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    if (active(ks, tile(ti))) {
+                        acc[ti][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bw[0][ks]),
+                                                                            cur[ti], acc[ti][0], 0, 0, 0);
+                        acc[ti][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bw[1][ks]),
+                                                                            cur[ti], acc[ti][1], 0, 0, 0);
+                    }
                 }
             }
             u32x4* dst = (u32x4*)(ctx.da2 + (size_t)f * 5184);
             const int c = 4 * chh + g;
 #pragma unroll
             for (int ti = 0; ti < 3; ++ti) {  // 3 stores per frame (nst above)
-                const int ri = (3 * ph + ti) * 16 + si;
+                const int ri = tile(ti) * 16 + si;
                 if (ri < 81) {
                     const s16x8 m = *(const s16x8*)(X + 16 * (ri + 96 * c + c3::zc(c)));
                     bf16x8 o;
@@ -1976,6 +1983,14 @@ __global__ __launch_bounds__(512, 2) void conv3_bwd_fr(const __bf16* __restrict_
 #endif
                 }
             }
+        };
+#ifdef FI_EXP_NODX
+        c3_frames(ctx, smem, 0, [&](const char* X, int f) {
+#else
+        c3_frames(ctx, smem, 3, [&](const char* X, int f) {
+#endif
+            if (ph) work(std::integral_constant<int, 1>{}, X, f);
+            else work(std::integral_constant<int, 0>{}, X, f);
         });
     }
 }

@@ -49,6 +49,14 @@ namespace fi {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
+// max of three through v_max3_f32 directly: fmaxf() under the kernels' IEEE mode makes hipcc
+// quiet every LDS-loaded operand first (one v_max_f32 x, x, x each), doubling the row-max cost
+__device__ __forceinline__ float vt_max3(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 struct VtArgs {
     int T, B, A;
     const float* __restrict__ pi;
@@ -187,9 +195,18 @@ struct VtLayout {
 // queue chunk (rows t0 .. t0+31) into ring slot `slot`; returns the pieces this wave issued
 // (pieces I0 <= i < I1 of this wave's list: logits pieces 0..GLOG-1, then its scalar piece;
 // the list is issued in groups between arithmetic so the TA drains between them)
+struct VtRsrc {  // buffer descriptors of the six input tensors (built once per workgroup)
+    fi_i32x4 pi, mu, act, rew, disc, val;
+};
+__device__ __forceinline__ VtRsrc vt_rsrc(const VtArgs& a) {
+    const uint32_t lbytes = (uint32_t)a.T * a.B * a.A * 4, sbytes = (uint32_t)a.T * a.B * 4;
+    return VtRsrc{make_rsrc(a.pi, lbytes), make_rsrc(a.mu, lbytes), make_rsrc(a.act, sbytes),
+                  make_rsrc(a.rew, sbytes), make_rsrc(a.disc, sbytes), make_rsrc(a.val, sbytes + a.B * 4)};
+}
+
 template <int A, int I0, int I1>
-__device__ __forceinline__ int vt_issue_chunk(const VtArgs& a, uint32_t lds0, int slot, int t0,
-                                              int b0, int w, int lane) {
+__device__ __forceinline__ int vt_issue_chunk(const VtArgs& a, const VtRsrc& rs, uint32_t lds0, int slot,
+                                              int t0, int b0, int w, int lane) {
     using L = VtLayout<A>;
     const uint32_t base = lds0 + (uint32_t)(slot * L::SLOT);
     const int first_row = t0 < 0 ? -t0 : 0;  // rows above hold t < 0: not needed
@@ -203,8 +220,10 @@ __device__ __forceinline__ int vt_issue_chunk(const VtArgs& a, uint32_t lds0, in
         const int q = jj * 1024 + 16 * lane;  // byte inside the tile
         const int tl = q / L::ROWB, cb = q - tl * L::ROWB;
         const int t = max(t0 + tl, 0);
-        const float* arr = j < L::PT ? a.pi : a.mu;
-        glds16((const char*)(arr + ((size_t)t * a.B + b0) * A) + cb, base + (j < L::PT ? 0 : L::LOGB) + jj * 1024);
+        // 32-bit buffer offsets (a (T, B, A) fp32 tensor is far below 4 GiB): no 64-bit
+        // address arithmetic per piece
+        blds16(j < L::PT ? rs.pi : rs.mu, (uint32_t)((t * a.B + b0) * A * 4 + cb),
+               base + (j < L::PT ? 0 : L::LOGB) + jj * 1024);
         ++n;
     }
     if (I1 > L::GLOG) {  // scalar tiles (TC rows x 8 columns x 4 B): wave w's piece holds 4/NW of them,
@@ -212,11 +231,17 @@ __device__ __forceinline__ int vt_issue_chunk(const VtArgs& a, uint32_t lds0, in
         constexpr int LPT = 16 * L::NW;  // lanes per tile
         const int s = w * (4 / L::NW) + lane / LPT;
         const int t = max(t0 + ((lane % LPT) >> 1), 0);
-        const char* arr = s == 0 ? (const char*)a.act
-                          : s == 1 ? (const char*)a.rew
-                          : s == 2 ? (const char*)a.disc
-                                   : (const char*)a.val;
-        glds16(arr + ((size_t)t * a.B + b0) * 4 + (lane & 1) * 16, base + 2 * L::LOGB + w * 1024);
+        // the piece's 4/NW tiles come from up to 4 tensors: one descriptor per tile, lanes select
+        const uint32_t off = (uint32_t)((t * a.B + b0) * 4 + (lane & 1) * 16);
+        if constexpr (L::NW == 4) {
+            blds16(w == 0 ? rs.act : w == 1 ? rs.rew : w == 2 ? rs.disc : rs.val, off, base + 2 * L::LOGB + w * 1024);
+        } else {
+            const char* arr = s == 0 ? (const char*)a.act
+                              : s == 1 ? (const char*)a.rew
+                              : s == 2 ? (const char*)a.disc
+                                       : (const char*)a.val;
+            glds16(arr + ((size_t)t * a.B + b0) * 4 + (lane & 1) * 16, base + 2 * L::LOGB + w * 1024);
+        }
         ++n;
     }
     return n;
@@ -242,7 +267,8 @@ __global__ __launch_bounds__(64 * VtLayout<A>::NW, VtLayout<A>::WPS) void vtrace
     if (tid < L::NB) a.dval[(size_t)T * B + b0 + tid] = 0.f;
 
     constexpr int NP = L::GLOG + 1, G1 = NP / 3, G2 = 2 * NP / 3;  // issue groups
-    int issued = vt_issue_chunk<A, 0, NP>(a, lds0, 0, T - L::TC, b0, w, lane);
+    const VtRsrc rs = vt_rsrc(a);
+    int issued = vt_issue_chunk<A, 0, NP>(a, rs, lds0, 0, T - L::TC, b0, w, lane);
     int mark = issued;  // VMEM ops issued once the chunk being waited for was queued
     const fi_vtrace_hparams hp = a.hp;
 
@@ -262,7 +288,7 @@ __global__ __launch_bounds__(64 * VtLayout<A>::NW, VtLayout<A>::WPS) void vtrace
         lds_barrier();  // B1: chunk k landed for every wave; slot (k+1)&1 fully consumed
         VT_STAMP();
         const bool more = k + 1 < nchunks;
-        if (more) issued += vt_issue_chunk<A, 0, G1>(a, lds0, slot ^ 1, t0 - L::TC, b0, w, lane);
+        if (more) issued += vt_issue_chunk<A, 0, G1>(a, rs, lds0, slot ^ 1, t0 - L::TC, b0, w, lane);
         VT_STAMP();
 #ifndef FI_VT_DMAONLY
         char* sl = smem + slot * L::SLOT;
@@ -293,11 +319,11 @@ __global__ __launch_bounds__(64 * VtLayout<A>::NW, VtLayout<A>::WPS) void vtrace
         const float vn = (tl == L::TC - 1) ? vnext : sval[(tl + 1) * L::NB + c];
         const float vrow0 = sval[c];  // V at this chunk's first row: next chunk's vnext
 
-        float mx = fmaxf(zp2[0].x, zp2[0].y), mm = fmaxf(zm2[0].x, zm2[0].y);
+        float mx = vt_max3(zp2[0].x, zp2[0].y, zp2[0].y), mm = vt_max3(zm2[0].x, zm2[0].y, zm2[0].y);
 #pragma unroll
         for (int i = 1; i < A / 2; ++i) {
-            mx = fmaxf(mx, fmaxf(zp2[i].x, zp2[i].y));
-            mm = fmaxf(mm, fmaxf(zm2[i].x, zm2[i].y));
+            mx = vt_max3(mx, zp2[i].x, zp2[i].y);
+            mm = vt_max3(mm, zm2[i].x, zm2[i].y);
         }
         const f32x2 nmx = {-mx * L2E, -mx * L2E}, nmm = {-mm * L2E, -mm * L2E};
         f32x2 e2[A / 2];
@@ -311,7 +337,7 @@ __global__ __launch_bounds__(64 * VtLayout<A>::NW, VtLayout<A>::WPS) void vtrace
             sz2 += e2[i] * zp2[i];
             sm2 += f32x2{VT_EXP2(am.x), VT_EXP2(am.y)};
         }
-        if (more) issued += vt_issue_chunk<A, G1, G2>(a, lds0, slot ^ 1, t0 - L::TC, b0, w, lane);
+        if (more) issued += vt_issue_chunk<A, G1, G2>(a, rs, lds0, slot ^ 1, t0 - L::TC, b0, w, lane);
         const float sp = sp2.x + sp2.y, sm = sm2.x + sm2.y;
         const float lse = mx + VT_LOG2(sp) * LN2, lsem = mm + VT_LOG2(sm) * LN2;
         const float inv = __builtin_amdgcn_rcpf(sp);
@@ -330,7 +356,7 @@ __global__ __launch_bounds__(64 * VtLayout<A>::NW, VtLayout<A>::WPS) void vtrace
             const float d2 = __shfl_down(d, s, 64), g2 = __shfl_down(gg, s, 64);
             if (lane + s < 64) { d = d + gg * d2; gg = gg * g2; }
         }
-        if (more) issued += vt_issue_chunk<A, G2, NP>(a, lds0, slot ^ 1, t0 - L::TC, b0, w, lane);
+        if (more) issued += vt_issue_chunk<A, G2, NP>(a, rs, lds0, slot ^ 1, t0 - L::TC, b0, w, lane);
         mark = issued;  // the wait for chunk k+1 ignores the stores issued after this point
         // wave total -> this wave's own first mu row (no other wave reads it)
         float* tot = (float*)(sl + L::LOGB) + (8 * w) * L::ROWF;
