@@ -10,7 +10,8 @@
 //   wgrad    dW[3136][512] = a3^T dh  (fp32 out, straight into the gradient blob)
 // All row-major; hipBLASLt is column-major, so each call computes the transposed product.
 // W is the bf16 copy of the fp32 master in the oracle's [3136][512] order.
-// Algorithms: the heuristic's top 16 candidates are timed once at creation, on operands filled
+// Algorithms: the heuristic's top 64 candidates are timed once at creation (16 missed a dgrad
+// kernel 17 % faster), on operands filled
 // with hashed bf16 values (the chip's clock under load depends on the data: candidates timed
 // on zero-filled buffers ranked differently from the step), and the fastest kept. The choice is
 // cached per GEMM shape for the life of the process, so every learner handle of one process
@@ -52,6 +53,10 @@ static std::string blt_err(const char* what, int st) { return std::string(what) 
 
 // shape -> index of the timed winner in the (deterministic) heuristic list
 using GemmKey = std::tuple<int, int, int, bool, bool, int, int>;
+#ifndef FI_BLT_CAND
+#define FI_BLT_CAND 64
+#endif
+constexpr int kCand = FI_BLT_CAND;  // heuristic candidates timed at creation
 static std::mutex g_algo_mu;
 static std::map<GemmKey, int> g_algo_choice;
 
@@ -73,9 +78,9 @@ static int make_gemm(FcBlasLt* F, FcGemm& G, int m, int n, int k, bool ta, bool 
     BLT(hipblasLtMatmulPreferenceCreate(&pref));
     BLT(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &F->wsb,
                                               sizeof(F->wsb)));
-    hipblasLtMatmulHeuristicResult_t res[16];
+    hipblasLtMatmulHeuristicResult_t res[kCand];
     int got = 0;
-    const int st = (int)hipblasLtMatmulAlgoGetHeuristic(F->h, G.desc, G.la, G.lb, G.ld, G.ld, pref, 16, res, &got);
+    const int st = (int)hipblasLtMatmulAlgoGetHeuristic(F->h, G.desc, G.la, G.lb, G.ld, G.ld, pref, kCand, res, &got);
     hipblasLtMatmulPreferenceDestroy(pref);
     if (st != 0 || got == 0) {
         set_error("hipBLASLt: no algorithm for the fc GEMM (m=" + std::to_string(m) + " n=" + std::to_string(n) +
