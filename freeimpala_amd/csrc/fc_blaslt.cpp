@@ -19,6 +19,8 @@
 #include <hip/hip_runtime.h>
 #include <hipblaslt/hipblaslt.h>
 
+#include <cstdio>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <string>
@@ -40,7 +42,9 @@ struct FcBlasLt {
     hipblasLtHandle_t h = nullptr;
     void* ws = nullptr;
     size_t wsb = 0;
-    FcGemm g[3];  // 0 forward, 1 dgrad, 2 wgrad
+    FcGemm g[4];  // 0 forward, 1 dgrad, 2 wgrad, 3 wgrad transposed (dW^T, then a transpose)
+    bool wgrad_t = false;    // run g[3] + transpose (the faster orientation at creation)
+    float* dwT = nullptr;    // [512][3136] fp32 scratch of the transposed wgrad
     int rows = 0;
 };
 
@@ -58,10 +62,11 @@ using GemmKey = std::tuple<int, int, int, bool, bool, int, int>;
 #endif
 constexpr int kCand = FI_BLT_CAND;  // heuristic candidates timed at creation
 static std::mutex g_algo_mu;
-static std::map<GemmKey, int> g_algo_choice;
+static std::map<GemmKey, std::pair<int, float>> g_algo_choice;  // -> (index, ms of 3 runs)
 
 static int make_gemm(FcBlasLt* F, FcGemm& G, int m, int n, int k, bool ta, bool tb, hipDataType dt_d,
-                     hipblasLtEpilogue_t epi, const void* A, const void* B, void* D, hipStream_t s) {
+                     hipblasLtEpilogue_t epi, const void* A, const void* B, void* D, hipStream_t s,
+                     float* best_ms = nullptr) {
     BLT(hipblasLtMatmulDescCreate(&G.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F));
     const hipblasOperation_t opa = ta ? HIPBLAS_OP_T : HIPBLAS_OP_N, opb = tb ? HIPBLAS_OP_T : HIPBLAS_OP_N;
     BLT(hipblasLtMatmulDescSetAttribute(G.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &opa, sizeof(opa)));
@@ -91,8 +96,9 @@ static int make_gemm(FcBlasLt* F, FcGemm& G, int m, int n, int k, bool ta, bool 
     {
         std::lock_guard<std::mutex> lk(g_algo_mu);
         auto it = g_algo_choice.find(key);
-        if (it != g_algo_choice.end() && it->second < got) {
-            G.algo = res[it->second].algo;
+        if (it != g_algo_choice.end() && it->second.first < got) {
+            G.algo = res[it->second.first].algo;
+            if (best_ms) *best_ms = it->second.second;
             return FI_OK;
         }
     }
@@ -128,10 +134,30 @@ static int make_gemm(FcBlasLt* F, FcGemm& G, int m, int n, int k, bool ta, bool 
         set_error("hipBLASLt: every fc GEMM candidate failed to launch");
         return FI_ERR_UNSUPPORTED;
     }
-    G.algo = res[bi].algo;
     std::lock_guard<std::mutex> lk(g_algo_mu);
-    g_algo_choice.emplace(key, bi);  // first timing wins for the whole process
-    G.algo = res[g_algo_choice[key]].algo;
+    g_algo_choice.emplace(key, std::make_pair(bi, best));  // first timing wins for the whole process
+    G.algo = res[g_algo_choice[key].first].algo;
+    if (best_ms) *best_ms = g_algo_choice[key].second;
+    return FI_OK;
+}
+
+// dW[3136][512] = transpose of dW^T[512][3136] (fp32, 32x32 tiles through LDS)
+__global__ __launch_bounds__(256) void transpose_f32_kernel(const float* __restrict__ src, int R, int C,
+                                                            float* __restrict__ dst) {
+    __shared__ float tile[32][33];
+    const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32, tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+#pragma unroll
+    for (int i = ty; i < 32; i += 8)
+        if (r0 + i < R && c0 + tx < C) tile[i][tx] = src[(size_t)(r0 + i) * C + c0 + tx];
+    __syncthreads();
+#pragma unroll
+    for (int i = ty; i < 32; i += 8)
+        if (c0 + i < C && r0 + tx < R) dst[(size_t)(c0 + i) * R + r0 + tx] = tile[tx][i];
+}
+
+static int transpose_f32(const float* src, int R, int C, float* dst, hipStream_t s) {
+    hipLaunchKernelGGL(transpose_f32_kernel, dim3((C + 31) / 32, (R + 31) / 32), dim3(256), 0, s, src, R, C, dst);
+    FI_HIP_CHECK(hipGetLastError());
     return FI_OK;
 }
 
@@ -158,7 +184,18 @@ FcBlasLt* fc_blaslt_create(int rows, const void* a3, const void* w, const void* 
     // column-major views of the row-major products (see the header comment)
     if (rc == FI_OK) rc = make_gemm(F, F->g[0], N, rows, K, false, false, HIP_R_16BF, HIPBLASLT_EPILOGUE_RELU_BIAS, w, a3, h, s);
     if (rc == FI_OK) rc = make_gemm(F, F->g[1], K, rows, N, true, false, HIP_R_16BF, HIPBLASLT_EPILOGUE_DEFAULT, w, dh, da3, s);
-    if (rc == FI_OK) rc = make_gemm(F, F->g[2], N, K, rows, false, true, HIP_R_32F, HIPBLASLT_EPILOGUE_DEFAULT, dh, a3, dw, s);
+    // wgrad in both orientations: dW (column-major N x K) directly, or dW^T (K x N) + a transpose
+    float t_direct = 0.f, t_trans = 0.f;
+    if (rc == FI_OK) rc = make_gemm(F, F->g[2], N, K, rows, false, true, HIP_R_32F, HIPBLASLT_EPILOGUE_DEFAULT, dh, a3, dw, s, &t_direct);
+    if (rc == FI_OK && hipMalloc((void**)&F->dwT, (size_t)K * N * sizeof(float)) != hipSuccess) {
+        set_error("fc: dW^T scratch allocation failed");
+        rc = FI_ERR_OOM;
+    }
+    if (rc == FI_OK) rc = make_gemm(F, F->g[3], K, N, rows, false, true, HIP_R_32F, HIPBLASLT_EPILOGUE_DEFAULT, a3, dh, F->dwT, s, &t_trans);
+    if (rc == FI_OK) F->wgrad_t = t_trans + 0.03f < t_direct;  // 3 timed runs + ~10 us per transpose
+    if (rc == FI_OK && std::getenv("FI_VERBOSE"))
+        std::fprintf(stderr, "[fc] wgrad 3 runs: direct %.3f ms, transposed %.3f ms -> %s\n", t_direct, t_trans,
+                     F->wgrad_t ? "transposed" : "direct");
     if (rc == FI_OK && hipStreamSynchronize(s) != hipSuccess) rc = FI_ERR_HIP;
     if (rc != FI_OK) {
         fc_blaslt_destroy(F);
@@ -176,6 +213,7 @@ void fc_blaslt_destroy(FcBlasLt* F) {
         if (G.desc) hipblasLtMatmulDescDestroy(G.desc);
     }
     if (F->ws) (void)hipFree(F->ws);
+    if (F->dwT) (void)hipFree(F->dwT);
     if (F->h) hipblasLtDestroy(F->h);
     delete F;
 }
@@ -197,6 +235,10 @@ int fc_blaslt_dgrad(FcBlasLt* F, const void* dh, const void* w, void* da3, hipSt
 }
 
 int fc_blaslt_wgrad(FcBlasLt* F, const void* a3, const void* dh, float* dw, hipStream_t s) {
+    if (F->wgrad_t) {
+        const int rc = run(F, F->g[3], a3, dh, F->dwT, s);
+        return rc ? rc : transpose_f32(F->dwT, 512, 3136, dw, s);
+    }
     return run(F, F->g[2], dh, a3, dw, s);
 }
 
