@@ -548,8 +548,11 @@ __global__ __launch_bounds__(256, 2) void heads_dgrad_valu(const float* __restri
                                                            const float* __restrict__ dval,
                                                            const float* __restrict__ wh,  // [512][O] fp32
                                                            const __bf16* __restrict__ h,
-                                                           __bf16* __restrict__ dh, int R, int TB) {
+                                                           __bf16* __restrict__ dh, int R, int TB,
+                                                           float* __restrict__ fcb_slab) {  // [grid][512]
+    __shared__ float cred[4][512];
     const int lane = threadIdx.x & 63, j0 = 8 * lane;
+    float cs8[8] = {};  // the fc bias gradient = column sums of dh, as stored (bf16)
     float w[8][O];
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj)
@@ -576,8 +579,16 @@ __global__ __launch_bounds__(256, 2) void heads_dgrad_valu(const float* __restri
         for (int jj = 0; jj < 8; ++jj) out[jj] = (float)hv[jj] > 0.f ? (__bf16)acc[jj] : (__bf16)0.f;
         *(bf16x8*)(dh + (size_t)r * 512 + j0) = out;
 #pragma unroll
+        for (int jj = 0; jj < 8; ++jj) cs8[jj] += (float)out[jj];
+#pragma unroll
         for (int o = 0; o < O; ++o) d[o] = dn[o];
     }
+    // the block's 4 waves hold the same columns: fixed-order sum, one partial row per block
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) cred[wave_id()][j0 + jj] = cs8[jj];
+    __syncthreads();
+    for (int c = threadIdx.x; c < 512; c += blockDim.x)
+        fcb_slab[(size_t)blockIdx.x * 512 + c] = ((cred[0][c] + cred[1][c]) + cred[2][c]) + cred[3][c];
 }
 
 template <int O>
@@ -647,9 +658,11 @@ static int heads_wgrad_launch(const float* dlog, const float* dval, const __bf16
     return FI_OK;
 }
 
+constexpr int kHeadsDgradGrid = 1024;
 static int heads_dgrad_launch(const float* dlog, const float* dval, const float* wh, const __bf16* h, __bf16* dh,
-                              int R, int TB, hipStream_t s) {
-    hipLaunchKernelGGL(heads_dgrad_valu<19>, dim3(1024), dim3(256), 0, s, dlog, dval, wh, h, dh, R, TB);
+                              int R, int TB, float* fcb_slab, hipStream_t s) {
+    hipLaunchKernelGGL(heads_dgrad_valu<19>, dim3(kHeadsDgradGrid), dim3(256), 0, s, dlog, dval, wh, h, dh, R, TB,
+                       fcb_slab);
     FI_HIP_CHECK(hipGetLastError());
     return FI_OK;
 }
@@ -879,20 +892,22 @@ int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, con
         FI_A("heads_wgrad", heads_wgrad_launch(dlogits, dvalue, I->h, slab, cs, N, I->TB, s));
         FI_A("reduce_slabs", reduce_slabs(slab, kHeadsGrid, (size_t)FCO * O, grads + o.hw, s));
         FI_A("reduce_slabs", reduce_slabs(cs, kHeadsGrid, (size_t)O, grads + o.hb, s));
-        FI_A("heads_dgrad", heads_dgrad_launch(dlogits, dvalue, I->params + o.hw, I->h, I->dh, N, I->TB, s));
+        // heads dgrad also leaves the fc bias partials (column sums of dh) in the slab
+        FI_A("heads_dgrad", heads_dgrad_launch(dlogits, dvalue, I->params + o.hw, I->h, I->dh, N, I->TB, slab, s));
+        FI_A("reduce_slabs", reduce_slabs(slab, kHeadsDgradGrid, (size_t)FCO, grads + o.fcb, s));
     } else {
         FI_A("heads_wgrad", (wgrad<128, 32, 4, 1>(RowsBf16{I->h, N, FCO}, dout, slab, cs, N, FCO, O, SPL_H, 1.f, s)));
         FI_A("reduce_slabs", reduce_slabs(slab, SPL_H, (size_t)FCO * O, grads + o.hw, s));
         FI_A("reduce_slabs", reduce_slabs(cs, SPL_H, (size_t)O, grads + o.hb, s));
         FI_A("heads_dgrad", (gemm<128, 128, 2, 2>(dout, RowsBf16{I->wb.hD, FCO, HP}, EpiMaskBf16{I->dh, I->h, FCO}, N, FCO,
                                    HP, s)));
+        FI_A("fc_bias", colsum_bf16(I->dh, N, FCO, slab, s));
+        FI_A("reduce_slabs", reduce_slabs(slab, kColsumSplits, (size_t)FCO, grads + o.fcb, s));
     }
     // fc: wgrad [3136][512] + bias, dgrad -> da3 (masked by a3)
     // fc (hipBLASLt): wgrad straight into the gradient blob, bias = column sums of dh,
     // dgrad -> da3 unmasked (conv3's backward applies the a3 ReLU mask as it loads da3)
     FI_A("fc_wgrad", fc_blaslt_wgrad(I->fc, I->a3, I->dh, grads + o.fcw, s));
-    FI_A("fc_bias", colsum_bf16(I->dh, N, FCO, slab, s));
-    FI_A("reduce_slabs", reduce_slabs(slab, kColsumSplits, (size_t)FCO, grads + o.fcb, s));
     FI_A("fc_dgrad", fc_blaslt_dgrad(I->fc, I->dh, I->wb.fcB, I->da3, s));
     // conv3: wgrad [576][64] + bias, dgrad -> da2 (masked by a2)
     if (I->fr) {
