@@ -27,6 +27,7 @@ sys.path.insert(0, ROOT)
 METRIC = "learner env-steps/sec (T×B/step) at T=100 B=4096, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}  # dense peaks (no sparsity)
+VT_REPLAYS = 100  # back-to-back V-trace launches per timing (the events' own overhead over 20 was ~2 %)
 
 
 def kernel_work(arch, T, B, A, D=128, H=256):
@@ -190,7 +191,7 @@ def main():
     kt = kernel_times(L)
     phases = L.phase_times()
     L.set_profiling(False)
-    vt_replay_ms = L.replay_vtrace(20)  # the scan kernel alone, back-to-back (see roof_vtrace)
+    vt_replay_ms = L.replay_vtrace(VT_REPLAYS)  # the scan kernel alone, back-to-back (see roof_vtrace)
     st = L.step_resident(stats=True)
 
     work = kernel_work(args.arch, T, B, A)
@@ -238,10 +239,10 @@ def main():
         },
         "roofline": roof(dominant) if dominant else None,
         # V-trace scan: ~20 us, so per-launch event brackets inside the step carry the dispatch
-        # latency; the burst of 20 back-to-back launches on the same resident tensors is the
+        # latency; the burst of VT_REPLAYS back-to-back launches on the same resident tensors is the
         # kernel's duration (agrees with rocprofv3's kernel-trace average)
         "roofline_vtrace": dict(roof("vtrace", vt_replay_ms) or {},
-                                method="HIP events around 20 back-to-back launches",
+                                method=f"HIP events around {VT_REPLAYS} back-to-back launches",
                                 in_step_event_ms=round(kt["vtrace"]["ms"], 5) if "vtrace" in kt else None),
         "kernel_ms_per_step": {k: round(v, 4) for k, v in sorted(per_step.items(), key=lambda x: -x[1])},
         "phase_ms": {k: round(v, 4) for k, v in phases.items() if k != "steps"},
