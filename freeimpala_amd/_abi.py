@@ -60,6 +60,9 @@ SIGNATURES = {
     "fi_learner_step": ([_P, C.POINTER(_P), C.c_size_t, C.c_size_t, C.POINTER(StepStats)], C.c_int),
     "fi_learner_step_async": ([_P, C.POINTER(_P), C.c_size_t, C.c_size_t], C.c_int),
     "fi_learner_wait": ([_P, C.POINTER(StepStats)], C.c_int),
+    "fi_learner_acquire_staging": ([_P, C.POINTER(_P), C.POINTER(C.c_size_t)], C.c_int),
+    "fi_learner_step_staged": ([_P, C.POINTER(StepStats)], C.c_int),
+    "fi_learner_step_staged_async": ([_P], C.c_int),
     "fi_learner_state_bytes": ([_P], C.c_size_t),
     "fi_learner_save_state": ([_P, _P, C.c_size_t], C.c_int),
     "fi_learner_load_state": ([_P, _P, C.c_size_t], C.c_int),

@@ -12,6 +12,9 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <new>
@@ -73,14 +76,20 @@ struct fi_learner {
     size_t slab_floats = 0;
     int splits = 1;
     AtariNet* atari = nullptr;
-    // host entry staging: two pinned buffers, so the host copy of batch k+1 overlaps the
-    // device step of batch k (fi_learner_step_async); each has an event marking the end of
-    // the H2D copy that reads it
+    // host entry staging, double-buffered on both sides of PCIe: the host copy of batch k+1
+    // into pinned2[s] and its H2D into rec_slot[s] (on copy_stream) overlap the device step
+    // of batch k (fi_learner_step_async). h2d_done[s] marks the end of the H2D that reads
+    // pinned2[s] / writes rec_slot[s]; ingest_done[s] the end of the ingest kernel that reads
+    // rec_slot[s].
     char* pinned2[2] = {nullptr, nullptr};
+    char* rec_slot[2] = {nullptr, nullptr};
     hipEvent_t h2d_done[2] = {nullptr, nullptr};
+    hipEvent_t ingest_done[2] = {nullptr, nullptr};
+    hipStream_t copy_stream = nullptr;
     int stage = 0;
+    int cur = 0;             // slot the next run_step ingests from
+    int acquired = -1;       // slot handed out by acquire_slot and not yet submitted
     bool in_flight = false;  // an async step was enqueued and not yet waited for
-    char* rec_dev = nullptr;
     size_t rec_bytes = 0;
     size_t rec_entry_bytes = 0;
     // data parallel
@@ -185,12 +194,14 @@ extern "C" void fi_learner_config_init(fi_learner_config* c) {
 static void destroy(fi_learner* l) {
     if (!l) return;
     if (l->stream) hipStreamSynchronize(l->stream);
+    if (l->copy_stream) hipStreamSynchronize(l->copy_stream);
     if (l->comm) ncclCommDestroy(l->comm);
     atari_destroy(l->atari);
     for (void* p : l->allocs) hipFree(p);
     for (int i = 0; i < 2; ++i) {
         if (l->pinned2[i]) hipHostFree(l->pinned2[i]);
         if (l->h2d_done[i]) hipEventDestroy(l->h2d_done[i]);
+        if (l->ingest_done[i]) hipEventDestroy(l->ingest_done[i]);
     }
     for (auto& e : l->ev)
         if (e) hipEventDestroy(e);
@@ -199,6 +210,7 @@ static void destroy(fi_learner* l) {
     if (l->ev_a) hipEventDestroy(l->ev_a);
     if (l->ev_b) hipEventDestroy(l->ev_b);
     if (l->stream) hipStreamDestroy(l->stream);
+    if (l->copy_stream) hipStreamDestroy(l->copy_stream);
     delete l;
 }
 
@@ -440,10 +452,15 @@ static int run_step(fi_learner* l, bool have_host_batch, fi_step_stats* out) {
     if (out) FI_HIP_CHECK(hipEventRecord(l->ev_a, l->stream));
     mark(l, FI_PHASE_INGEST);
     if (have_host_batch) {
-        Tag t(l, "ingest");
-        FI_TRY(ingest_launch(l->rec_dev, l->T, l->B, l->A, l->D, l->rec_entry_bytes,
-                             l->cfg.arch == FI_ARCH_MLP ? l->obs : nullptr, l->mu, l->act, l->rew,
-                             l->disc, l->stream));
+        const int s = l->cur;
+        FI_HIP_CHECK(hipStreamWaitEvent(l->stream, l->h2d_done[s], 0));
+        {
+            Tag t(l, "ingest");
+            FI_TRY(ingest_launch(l->rec_slot[s], l->T, l->B, l->A, l->D, l->rec_entry_bytes,
+                                 l->cfg.arch == FI_ARCH_MLP ? l->obs : nullptr, l->mu, l->act,
+                                 l->rew, l->disc, l->stream));
+        }
+        FI_HIP_CHECK(hipEventRecord(l->ingest_done[s], l->stream));
     }
     mark(l, FI_PHASE_FORWARD);
     if (l->cfg.arch == FI_ARCH_MLP) FI_TRY(mlp_forward(l));
@@ -558,48 +575,102 @@ static void parallel_copy(char* dst, const void* const* entries, size_t n, size_
     for (auto& t : th) t.join();
 }
 
-// stage M host entries (only their first T+1 records) into the next pinned buffer and
-// enqueue its H2D copy; returns once the host copy is done (the entries may then be freed)
-static int stage_entries(fi_learner* l, const void* const* entries, size_t n_entries, size_t entry_bytes) {
-    FI_REQUIRE(l && entries, "step: null argument");
+// Host staging, double-buffered: acquire_slot() hands out the next pinned buffer once the
+// H2D that last read it is done; submit_slot() enqueues its H2D on the copy stream (after the
+// ingest that last read the device slot) and makes it the batch the next run_step ingests.
+static int ensure_staging(fi_learner* l) {
     FI_REQUIRE(l->cfg.arch == FI_ARCH_MLP,
                "step: host trajectory records carry <=128-float observations (MLP); the Atari "
                "config is device-synthetic (fi_learner_synth_batch + fi_learner_step_resident)");
+    const size_t need = (size_t)(l->T + 1) * FI_RECORD_BYTES;
+    const size_t bytes = (size_t)l->B * need;
+    if (bytes <= l->rec_bytes) return FI_OK;
+    FI_HIP_CHECK(hipStreamSynchronize(l->stream));
+    if (l->copy_stream) FI_HIP_CHECK(hipStreamSynchronize(l->copy_stream));
+    else FI_HIP_CHECK(hipStreamCreateWithFlags(&l->copy_stream, hipStreamNonBlocking));
+    for (int i = 0; i < 2; ++i) {
+        if (l->pinned2[i]) hipHostFree(l->pinned2[i]);
+        l->pinned2[i] = nullptr;
+        if (l->rec_slot[i]) {
+            hipFree(l->rec_slot[i]);
+            l->allocs.erase(std::find(l->allocs.begin(), l->allocs.end(), (void*)l->rec_slot[i]));
+        }
+        l->rec_slot[i] = nullptr;
+    }
+    l->rec_bytes = 0;
+    for (int i = 0; i < 2; ++i) {
+        FI_HIP_CHECK(hipHostMalloc((void**)&l->pinned2[i], bytes, hipHostMallocDefault));
+        FI_TRY(dalloc(l, (void**)&l->rec_slot[i], bytes));
+        if (!l->h2d_done[i]) FI_HIP_CHECK(hipEventCreateWithFlags(&l->h2d_done[i], hipEventDisableTiming));
+        if (!l->ingest_done[i]) FI_HIP_CHECK(hipEventCreateWithFlags(&l->ingest_done[i], hipEventDisableTiming));
+        FI_HIP_CHECK(hipEventRecord(l->h2d_done[i], l->copy_stream));
+        FI_HIP_CHECK(hipEventRecord(l->ingest_done[i], l->stream));
+    }
+    l->rec_bytes = bytes;
+    l->rec_entry_bytes = need;
+    return FI_OK;
+}
+
+static bool stage_timing() {
+    static const bool on = std::getenv("FI_STAGE_TIMING") != nullptr;
+    return on;
+}
+
+static int acquire_slot(fi_learner* l, int* slot) {
+    FI_TRY(ensure_staging(l));
+    if (l->acquired < 0) {
+        const auto t0 = std::chrono::steady_clock::now();
+        // pinned2[s] is free once the H2D that read it (two steps ago) is done
+        FI_HIP_CHECK(hipEventSynchronize(l->h2d_done[l->stage]));
+        l->acquired = l->stage;
+        l->stage ^= 1;
+        if (stage_timing())
+            std::fprintf(stderr, "[fi stage] slot %d wait %.3f ms\n", l->acquired,
+                         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    }
+    *slot = l->acquired;
+    return FI_OK;
+}
+
+static int submit_slot(fi_learner* l) {
+    FI_REQUIRE(l->acquired >= 0, "step_staged: no staging slot acquired (fi_learner_acquire_staging)");
+    const int s = l->acquired;
+    // the device slot is rewritten after the ingest kernel of two steps ago has read it; the
+    // copy runs on its own stream, beside the device step of the previous batch
+    FI_HIP_CHECK(hipStreamWaitEvent(l->copy_stream, l->ingest_done[s], 0));
+    FI_HIP_CHECK(hipMemcpyAsync(l->rec_slot[s], l->pinned2[s], l->rec_bytes, hipMemcpyHostToDevice,
+                                l->copy_stream));
+    FI_HIP_CHECK(hipEventRecord(l->h2d_done[s], l->copy_stream));
+    l->cur = s;
+    l->acquired = -1;
+    return FI_OK;
+}
+
+// stage M host entries (only their first T+1 records) through the next pinned buffer; returns
+// once the host copy is done (the entries may then be freed)
+static int stage_entries(fi_learner* l, const void* const* entries, size_t n_entries, size_t entry_bytes) {
+    FI_REQUIRE(l && entries, "step: null argument");
     FI_REQUIRE(n_entries == (size_t)l->B, "step: n_entries must equal the configured batch");
     const size_t need = (size_t)(l->T + 1) * FI_RECORD_BYTES;
     FI_REQUIRE(entry_bytes >= need, "step: entry_bytes < (T+1)*1024");
     for (size_t i = 0; i < n_entries; ++i) FI_REQUIRE(entries[i], "step: null entry");
     FI_HIP_CHECK(hipSetDevice(l->dev));
-    const size_t bytes = n_entries * need;
-    if (bytes > l->rec_bytes) {
-        FI_HIP_CHECK(hipStreamSynchronize(l->stream));
-        for (int i = 0; i < 2; ++i) {
-            if (l->pinned2[i]) hipHostFree(l->pinned2[i]);
-            l->pinned2[i] = nullptr;
-        }
-        if (l->rec_dev) {
-            hipFree(l->rec_dev);
-            l->allocs.erase(std::find(l->allocs.begin(), l->allocs.end(), (void*)l->rec_dev));
-        }
-        l->rec_dev = nullptr;
-        l->rec_bytes = 0;
-        for (int i = 0; i < 2; ++i) {
-            FI_HIP_CHECK(hipHostMalloc((void**)&l->pinned2[i], bytes, hipHostMallocDefault));
-            if (!l->h2d_done[i]) FI_HIP_CHECK(hipEventCreateWithFlags(&l->h2d_done[i], hipEventDisableTiming));
-            FI_HIP_CHECK(hipEventRecord(l->h2d_done[i], l->stream));
-        }
-        FI_TRY(dalloc(l, (void**)&l->rec_dev, bytes));
-        l->rec_bytes = bytes;
-    }
-    const int s = l->stage;
-    l->stage ^= 1;
-    // the H2D that last read this pinned buffer (two steps ago) must be done before reuse
-    FI_HIP_CHECK(hipEventSynchronize(l->h2d_done[s]));
+    int s = 0;
+    FI_TRY(acquire_slot(l, &s));
+    const auto t0 = std::chrono::steady_clock::now();
     parallel_copy(l->pinned2[s], entries, n_entries, need, need);
-    // rec_dev is rewritten in stream order, after the previous step's ingest kernel read it
-    FI_HIP_CHECK(hipMemcpyAsync(l->rec_dev, l->pinned2[s], bytes, hipMemcpyHostToDevice, l->stream));
-    FI_HIP_CHECK(hipEventRecord(l->h2d_done[s], l->stream));
-    l->rec_entry_bytes = need;
+    if (stage_timing()) {
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        std::fprintf(stderr, "[fi stage] slot %d copy %.3f ms (%.1f GB/s)\n", s, ms, l->rec_bytes / 1e6 / ms);
+    }
+    return submit_slot(l);
+}
+
+// a synchronous step: returns when the device step has completed, statistics or not
+static int step_and_wait(fi_learner* l, fi_step_stats* out) {
+    l->in_flight = false;
+    FI_TRY(run_step(l, true, out));
+    if (!out) FI_HIP_CHECK(hipStreamSynchronize(l->stream));
     return FI_OK;
 }
 
@@ -607,8 +678,7 @@ extern "C" int fi_learner_step(fi_learner* l, const void* const* entries, size_t
                                size_t entry_bytes, fi_step_stats* out) {
     try {
         FI_TRY(stage_entries(l, entries, n_entries, entry_bytes));
-        l->in_flight = false;
-        return run_step(l, true, out ? out : nullptr);
+        return step_and_wait(l, out);
     } catch (const std::exception& e) {
         return fail(FI_ERR_STATE, std::string("step: ") + e.what());
     }
@@ -623,6 +693,44 @@ extern "C" int fi_learner_step_async(fi_learner* l, const void* const* entries, 
         return FI_OK;
     } catch (const std::exception& e) {
         return fail(FI_ERR_STATE, std::string("step_async: ") + e.what());
+    }
+}
+
+extern "C" int fi_learner_acquire_staging(fi_learner* l, void** dst, size_t* entry_stride) {
+    FI_REQUIRE(l && dst, "acquire_staging: null argument");
+    try {
+        FI_HIP_CHECK(hipSetDevice(l->dev));
+        int s = 0;
+        FI_TRY(acquire_slot(l, &s));
+        *dst = l->pinned2[s];
+        if (entry_stride) *entry_stride = l->rec_entry_bytes;
+        return FI_OK;
+    } catch (const std::exception& e) {
+        return fail(FI_ERR_STATE, std::string("acquire_staging: ") + e.what());
+    }
+}
+
+extern "C" int fi_learner_step_staged(fi_learner* l, fi_step_stats* out) {
+    FI_REQUIRE(l, "step_staged: null learner");
+    try {
+        FI_HIP_CHECK(hipSetDevice(l->dev));
+        FI_TRY(submit_slot(l));
+        return step_and_wait(l, out);
+    } catch (const std::exception& e) {
+        return fail(FI_ERR_STATE, std::string("step_staged: ") + e.what());
+    }
+}
+
+extern "C" int fi_learner_step_staged_async(fi_learner* l) {
+    FI_REQUIRE(l, "step_staged_async: null learner");
+    try {
+        FI_HIP_CHECK(hipSetDevice(l->dev));
+        FI_TRY(submit_slot(l));
+        FI_TRY(run_step(l, true, nullptr));
+        l->in_flight = true;
+        return FI_OK;
+    } catch (const std::exception& e) {
+        return fail(FI_ERR_STATE, std::string("step_staged_async: ") + e.what());
     }
 }
 

@@ -19,6 +19,23 @@ from ._abi import check, lib
 from . import hip
 
 
+class HostBatch:
+    """M host entries pinned down once as a C pointer table (what Learner::step hands the ABI:
+    `const void* const* entries`). Building the table costs ~1 us per entry in Python, so a
+    caller that steps the same buffers repeatedly builds it once."""
+
+    def __init__(self, batch: Sequence[bytes | bytearray | np.ndarray]):
+        self.bufs = [np.frombuffer(e, dtype=np.uint8) if not isinstance(e, np.ndarray)
+                     else np.ascontiguousarray(e).view(np.uint8).ravel() for e in batch]
+        self.n = len(self.bufs)
+        self.entry_bytes = min(b.nbytes for b in self.bufs) if self.bufs else 0
+        self.ptrs = (C.c_void_p * self.n)(*[b.ctypes.data for b in self.bufs])
+
+
+def _as_host_batch(batch) -> HostBatch:
+    return batch if isinstance(batch, HostBatch) else HostBatch(batch)
+
+
 class DeviceLearner:
     def __init__(self, arch: str = "mlp", seq_len: int = 100, batch: int = 32,
                  num_actions: int = 18, obs_dim: int = 128, hidden: int = 256,
@@ -49,26 +66,38 @@ class DeviceLearner:
         return int(lib().fi_learner_entry_bytes(self._h))
 
     # --- the step
-    def step(self, batch: Sequence[bytes | bytearray | np.ndarray], stats: bool = True) -> dict:
+    def step(self, batch: Sequence[bytes | bytearray | np.ndarray] | HostBatch,
+             stats: bool = True) -> dict:
         """Learner::step(player, batch): batch = M SharedBuffer entries (host bytes)."""
-        bufs = [np.frombuffer(e, dtype=np.uint8) if not isinstance(e, np.ndarray)
-                else np.ascontiguousarray(e).view(np.uint8).ravel() for e in batch]
-        n = len(bufs)
-        eb = min(b.nbytes for b in bufs) if bufs else 0
-        ptrs = (C.c_void_p * n)(*[b.ctypes.data for b in bufs])
+        hb = _as_host_batch(batch)
         st = _abi.StepStats()
-        check(lib().fi_learner_step(self._h, ptrs, n, eb, C.byref(st) if stats else None),
-              "fi_learner_step")
+        check(lib().fi_learner_step(self._h, hb.ptrs, hb.n, hb.entry_bytes,
+                                    C.byref(st) if stats else None), "fi_learner_step")
         return st.as_dict() if stats else {}
 
-    def step_async(self, batch: Sequence[bytes | bytearray | np.ndarray]) -> None:
+    def step_async(self, batch: Sequence[bytes | bytearray | np.ndarray] | HostBatch) -> None:
         """Stage the entries (copied before return) and enqueue the step; see wait()."""
-        bufs = [np.frombuffer(e, dtype=np.uint8) if not isinstance(e, np.ndarray)
-                else np.ascontiguousarray(e).view(np.uint8).ravel() for e in batch]
-        n = len(bufs)
-        eb = min(b.nbytes for b in bufs) if bufs else 0
-        ptrs = (C.c_void_p * n)(*[b.ctypes.data for b in bufs])
-        check(lib().fi_learner_step_async(self._h, ptrs, n, eb), "fi_learner_step_async")
+        hb = _as_host_batch(batch)
+        check(lib().fi_learner_step_async(self._h, hb.ptrs, hb.n, hb.entry_bytes),
+              "fi_learner_step_async")
+
+    def acquire_staging(self) -> np.ndarray:
+        """The next pinned staging buffer as a writable (B, entry_bytes) uint8 view
+        (SharedBuffer::readBatchInto's destination); valid until it is submitted."""
+        dst, stride = C.c_void_p(), C.c_size_t()
+        check(lib().fi_learner_acquire_staging(self._h, C.byref(dst), C.byref(stride)),
+              "fi_learner_acquire_staging")
+        buf = (C.c_uint8 * (self.B * stride.value)).from_address(dst.value)
+        return np.frombuffer(buf, np.uint8).reshape(self.B, stride.value)
+
+    def step_staged(self, stats: bool = True) -> dict:
+        st = _abi.StepStats()
+        check(lib().fi_learner_step_staged(self._h, C.byref(st) if stats else None),
+              "fi_learner_step_staged")
+        return st.as_dict() if stats else {}
+
+    def step_staged_async(self) -> None:
+        check(lib().fi_learner_step_staged_async(self._h), "fi_learner_step_staged_async")
 
     def wait(self) -> dict:
         st = _abi.StepStats()

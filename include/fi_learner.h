@@ -113,6 +113,19 @@ int fi_learner_step_resident(fi_learner* l, fi_step_stats* out);
 int fi_learner_step_async(fi_learner* l, const void* const* entries, size_t n_entries,
                           size_t entry_bytes);
 int fi_learner_wait(fi_learner* l, fi_step_stats* out);
+/* Zero-copy staging (a SharedBuffer::readBatchInto(pinned dst)
+ * replacing readBatch's per-entry vector copies, data_structures.h:286-293).
+ * fi_learner_acquire_staging returns the next of the two pinned staging buffers, once the
+ * H2D that last read it has completed: cfg.batch entries, entry i at dst + i*entry_stride,
+ * entry_stride = fi_learner_entry_bytes(). The caller copies the first entry_stride bytes of
+ * each entry there (e.g. under the SharedBuffer mutex) and submits the buffer with
+ * fi_learner_step_staged (returns when the step is done) or fi_learner_step_staged_async
+ * (returns once enqueued; fi_learner_wait as above). The H2D runs on a copy stream beside
+ * the previous device step. Acquiring again before submitting returns the same buffer;
+ * submitting without an acquired buffer is FI_ERR_INVALID. MLP configuration only.       */
+int fi_learner_acquire_staging(fi_learner* l, void** dst, size_t* entry_stride);
+int fi_learner_step_staged(fi_learner* l, fi_step_stats* out);
+int fi_learner_step_staged_async(fi_learner* l);
 int fi_learner_synth_batch(fi_learner* l, uint64_t seed, int32_t b_global, int32_t b_offset);
 
 /* ---- parameter publication / resume (ModelManager::updateModel, Model::loadFromDisk) - */

@@ -183,6 +183,28 @@ public:
             return fail(player_index, fi_last_error());
         return true;
     }
+    // Zero-copy step: fill(dst, entry_stride, n) writes n entries straight into the pinned
+    // staging buffer (SharedBuffer::readBatchInto, under the buffer's own mutex) and returns
+    // false when there is no batch (draining, data_structures.h:278-280): then nothing is
+    // submitted and the same buffer is handed out next time. async as in step_async.
+    template <class Fill>
+    bool step_staged(size_t player_index, Fill&& fill, bool async = false) {
+        if (player_index >= handles_.size()) return fail(0, "player_index out of range");
+        fi_learner* h = handles_[player_index];
+        void* dst = nullptr;
+        size_t stride = 0;
+        if (fi_learner_acquire_staging(h, &dst, &stride) != FI_OK) return fail(player_index, fi_last_error());
+        if (!fill(static_cast<char*>(dst), stride, cfg_.batch_size)) return false;
+        if (async) {
+            if (fi_learner_step_staged_async(h) != FI_OK) return fail(player_index, fi_last_error());
+            return true;
+        }
+        fi_step_stats st{};
+        if (fi_learner_step_staged(h, &st) != FI_OK) return fail(player_index, fi_last_error());
+        stats_[player_index] = st;
+        return true;
+    }
+
     bool wait(size_t p) {
         if (p >= handles_.size()) return fail(0, "player_index out of range");
         fi_step_stats st{};

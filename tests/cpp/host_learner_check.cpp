@@ -154,6 +154,22 @@ static int gpu_mode(const std::string& out) {
     CHECK(!L.last_error(0).empty());
     CHECK(L.step(0, batch));
 
+    // zero-copy staging (SharedBuffer::readBatchInto): a drained buffer submits nothing; then
+    // player 1 takes its second step from the staging buffer and must match player 0's second
+    // step (which went through the entry-pointer path) bit for bit
+    CHECK(!L.step_staged(1, [](char*, size_t, size_t) { return false; }));
+    uint64_t vd = 0;
+    std::vector<char> pd;
+    CHECK(L.publish(1, pd, vd) && vd == v0 + 1);
+    CHECK(L.step_staged(1, [&](char* dst, size_t stride, size_t n) {
+        if (n != batch.size() || stride > batch[0].size()) return false;
+        for (size_t i = 0; i < n; ++i) std::memcpy(dst + i * stride, batch[i].data(), stride);
+        return true;
+    }));
+    std::vector<char> p2a, p2b;
+    CHECK(L.publish(0, p2a, va) && L.publish(1, p2b, vb));
+    CHECK(va == v0 + 2 && vb == v0 + 2 && p2a == p2b);
+
     std::vector<char> flat;
     for (const auto& e : batch) flat.insert(flat.end(), e.begin(), e.end());
     std::ofstream(out + "/batch.bin", std::ios::binary).write(flat.data(), (std::streamsize)flat.size());

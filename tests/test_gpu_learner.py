@@ -191,12 +191,13 @@ def test_bad_arguments_fail_loudly():
 
 
 def test_async_step_matches_sync_steps(orc):
-    """fi_learner_step_async x2 (entries freed right after each call) then wait == two
+    """fi_learner_step_async x4 (entries freed right after each call; both staging slots are
+    reused, so the H2D of batch k+2 must wait for the ingest of batch k) then wait == four
     synchronous steps on the same batches: same parameters, same last statistics."""
     from freeimpala_amd.learner import pack_records
     T, B = 6, 32
     batches = []
-    for seed in (21, 22):
+    for seed in (21, 22, 23, 24):
         b = orc.synth_batch(seed, T=T, B=B, A=18, D=128)
         batches.append(pack_records(b["obs"], b["mu"], b["actions"], b["rewards"], b["discounts"],
                                     entry_size=T + 1))
@@ -209,7 +210,40 @@ def test_async_step_matches_sync_steps(orc):
         del ent  # the call copied them
     s2 = L2.wait()
     np.testing.assert_array_equal(L1.get_params(), L2.get_params())
-    assert s1["total_loss"] == s2["total_loss"] and s1["version"] == s2["version"] == 2
+    assert s1["total_loss"] == s2["total_loss"] and s1["version"] == s2["version"] == 4
+
+
+def test_staged_steps_match_entry_steps(orc):
+    """Zero-copy staging: batches written straight into the acquired pinned buffer (what
+    SharedBuffer::readBatchInto would do), submitted sync and async, give the same parameters
+    and statistics as fi_learner_step on the same entries. Submitting without an acquired
+    buffer is an error that leaves the handle usable."""
+    from freeimpala_amd._abi import FiError
+    from freeimpala_amd.learner import pack_records
+    T, B = 6, 32
+    batches = []
+    for seed in (31, 32, 33, 34, 35):
+        b = orc.synth_batch(seed, T=T, B=B, A=18, D=128)
+        batches.append(pack_records(b["obs"], b["mu"], b["actions"], b["rewards"], b["discounts"],
+                                    entry_size=T + 2))  # one spare record: S > T+1
+    L1, L2 = mk(T=T, B=B, seed=4, optimizer="adam"), mk(T=T, B=B, seed=4, optimizer="adam")
+    for e in batches:
+        s1 = L1.step(e)
+    with pytest.raises(FiError):
+        L2.step_staged()
+    for i, e in enumerate(batches):
+        dst = L2.acquire_staging()
+        assert dst.shape == (B, (T + 1) * 1024)
+        assert L2.acquire_staging().ctypes.data == dst.ctypes.data  # same buffer until submitted
+        for j, x in enumerate(e):
+            dst[j] = np.frombuffer(x, np.uint8)[:dst.shape[1]]
+        if i == 0:
+            L2.step_staged(stats=False)
+        else:
+            L2.step_staged_async()
+    s2 = L2.wait()
+    np.testing.assert_array_equal(L1.get_params(), L2.get_params())
+    assert s1["total_loss"] == s2["total_loss"] and s1["version"] == s2["version"] == 5
 
 
 def test_state_checkpoint_resume_is_bit_exact():
