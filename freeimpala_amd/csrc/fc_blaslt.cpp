@@ -42,9 +42,12 @@ struct FcBlasLt {
     hipblasLtHandle_t h = nullptr;
     void* ws = nullptr;
     size_t wsb = 0;
-    FcGemm g[4];  // 0 forward, 1 dgrad, 2 wgrad, 3 wgrad transposed (dW^T, then a transpose)
-    bool wgrad_t = false;    // run g[3] + transpose (the faster orientation at creation)
+    FcGemm g[5];  // 0 forward, 1 dgrad, 2 wgrad, 3 wgrad transposed (dW^T, then a transpose),
+                  // 4 wgrad split over row blocks (a strided batch of partial dW, then a sum)
+    int wgrad_mode = 0;      // 0 direct, 1 transposed, 2 split (the fastest at creation)
     float* dwT = nullptr;    // [512][3136] fp32 scratch of the transposed wgrad
+    float* dwS = nullptr;    // [split][3136][512] fp32 partials of the split wgrad
+    int split = 0;
     int rows = 0;
 };
 
@@ -56,7 +59,7 @@ static std::string blt_err(const char* what, int st) { return std::string(what) 
     } while (0)
 
 // shape -> index of the timed winner in the (deterministic) heuristic list
-using GemmKey = std::tuple<int, int, int, bool, bool, int, int>;
+using GemmKey = std::tuple<int, int, int, bool, bool, int, int, int>;
 #ifndef FI_BLT_CAND
 #define FI_BLT_CAND 64
 #endif
@@ -66,7 +69,7 @@ static std::map<GemmKey, std::pair<int, float>> g_algo_choice;  // -> (index, ms
 
 static int make_gemm(FcBlasLt* F, FcGemm& G, int m, int n, int k, bool ta, bool tb, hipDataType dt_d,
                      hipblasLtEpilogue_t epi, const void* A, const void* B, void* D, hipStream_t s,
-                     float* best_ms = nullptr) {
+                     float* best_ms = nullptr, int batch = 1) {
     BLT(hipblasLtMatmulDescCreate(&G.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F));
     const hipblasOperation_t opa = ta ? HIPBLAS_OP_T : HIPBLAS_OP_N, opb = tb ? HIPBLAS_OP_T : HIPBLAS_OP_N;
     BLT(hipblasLtMatmulDescSetAttribute(G.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &opa, sizeof(opa)));
@@ -79,6 +82,14 @@ static int make_gemm(FcBlasLt* F, FcGemm& G, int m, int n, int k, bool ta, bool 
     BLT(hipblasLtMatrixLayoutCreate(&G.la, HIP_R_16BF, ta ? k : m, ta ? m : k, ta ? k : m));
     BLT(hipblasLtMatrixLayoutCreate(&G.lb, HIP_R_16BF, tb ? n : k, tb ? k : n, tb ? n : k));
     BLT(hipblasLtMatrixLayoutCreate(&G.ld, dt_d, m, n, m));
+    if (batch > 1) {  // batch i = the i-th block of k (rows); D_i = its partial product
+        const int32_t bc = batch;
+        const int64_t sa = (int64_t)m * k, sb = (int64_t)n * k, sd = (int64_t)m * n;
+        for (auto [L, st] : {std::make_pair(G.la, sa), std::make_pair(G.lb, sb), std::make_pair(G.ld, sd)}) {
+            BLT(hipblasLtMatrixLayoutSetAttribute(L, HIPBLASLT_MATRIX_LAYOUT_BATCH_COUNT, &bc, sizeof(bc)));
+            BLT(hipblasLtMatrixLayoutSetAttribute(L, HIPBLASLT_MATRIX_LAYOUT_STRIDED_BATCH_OFFSET, &st, sizeof(st)));
+        }
+    }
     hipblasLtMatmulPreference_t pref;
     BLT(hipblasLtMatmulPreferenceCreate(&pref));
     BLT(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &F->wsb,
@@ -92,7 +103,7 @@ static int make_gemm(FcBlasLt* F, FcGemm& G, int m, int n, int k, bool ta, bool 
                   " k=" + std::to_string(k) + ")");
         return FI_ERR_UNSUPPORTED;
     }
-    const GemmKey key{m, n, k, ta, tb, (int)dt_d, (int)epi};
+    const GemmKey key{m, n, k, ta, tb, (int)dt_d, (int)epi, batch};
     {
         std::lock_guard<std::mutex> lk(g_algo_mu);
         auto it = g_algo_choice.find(key);
@@ -161,6 +172,21 @@ static int transpose_f32(const float* src, int R, int C, float* dst, hipStream_t
     return FI_OK;
 }
 
+static int time_reduce(const float* slab, int S, size_t count, float* out, hipStream_t s, float* ms) {
+    hipEvent_t e0, e1;
+    FI_HIP_CHECK(hipEventCreate(&e0));
+    FI_HIP_CHECK(hipEventCreate(&e1));
+    int rc = FI_OK;
+    if (hipEventRecord(e0, s) != hipSuccess) rc = FI_ERR_HIP;
+    for (int i = 0; i < 3 && rc == FI_OK; ++i) rc = reduce_slabs(slab, S, count, out, s);
+    if (rc == FI_OK && (hipEventRecord(e1, s) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+                        hipEventElapsedTime(ms, e0, e1) != hipSuccess))
+        rc = FI_ERR_HIP;
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    return rc;
+}
+
 FcBlasLt* fc_blaslt_create(int rows, const void* a3, const void* w, const void* dh, void* h, void* da3,
                            float* dw, hipStream_t s) {
     FcBlasLt* F = new FcBlasLt();
@@ -192,10 +218,59 @@ FcBlasLt* fc_blaslt_create(int rows, const void* a3, const void* w, const void* 
         rc = FI_ERR_OOM;
     }
     if (rc == FI_OK) rc = make_gemm(F, F->g[3], K, N, rows, false, true, HIP_R_32F, HIPBLASLT_EPILOGUE_DEFAULT, a3, dh, F->dwT, s, &t_trans);
-    if (rc == FI_OK) F->wgrad_t = t_trans + 0.03f < t_direct;  // 3 timed runs + ~10 us per transpose
+    // split wgrad: S row blocks as one strided-batched GEMM (S partial dW), summed by
+    // reduce_slabs in a fixed order; S from FI_FC_SPLIT, or the fastest of 8 / 16 / 32 / 64
+    float t_split = 1e30f;
+    if (rc == FI_OK) {
+        const char* e = std::getenv("FI_FC_SPLIT");
+        const int fixed = e ? std::atoi(e) : 0;
+        for (int S : {8, 16, 32, 64}) {
+            if (fixed > 0 && S != fixed) continue;
+            if (rows % S || rows / S < 2048) continue;
+            float* slab = nullptr;
+            if (hipMalloc((void**)&slab, (size_t)S * K * N * sizeof(float)) != hipSuccess) break;
+            FcGemm G;
+            float t = 0.f;
+            int r2 = make_gemm(F, G, N, K, rows / S, false, true, HIP_R_32F, HIPBLASLT_EPILOGUE_DEFAULT, dh, a3,
+                               slab, s, &t, S);
+            float tr = 0.f;  // + the partial sum: 3 runs, as the GEMM timing
+            if (r2 == FI_OK) r2 = time_reduce(slab, S, (size_t)K * N, dw, s, &tr);
+            t += tr;
+            if (std::getenv("FI_VERBOSE"))
+                std::fprintf(stderr, "[fc] wgrad split %d, 3 runs incl. sum: %.3f ms\n", S, t);
+            if (r2 == FI_OK && t < t_split) {
+                t_split = t;
+                for (FcGemm* X : {&F->g[4]}) {
+                    if (X->la) hipblasLtMatrixLayoutDestroy(X->la);
+                    if (X->lb) hipblasLtMatrixLayoutDestroy(X->lb);
+                    if (X->ld) hipblasLtMatrixLayoutDestroy(X->ld);
+                    if (X->desc) hipblasLtMatmulDescDestroy(X->desc);
+                }
+                F->g[4] = G;
+                if (F->dwS) (void)hipFree(F->dwS);
+                F->dwS = slab;
+                F->split = S;
+            } else {
+                if (G.la) hipblasLtMatrixLayoutDestroy(G.la);
+                if (G.lb) hipblasLtMatrixLayoutDestroy(G.lb);
+                if (G.ld) hipblasLtMatrixLayoutDestroy(G.ld);
+                if (G.desc) hipblasLtMatmulDescDestroy(G.desc);
+                (void)hipFree(slab);
+            }
+        }
+    }
+    if (rc == FI_OK) {
+        const float tt = t_trans + 0.03f;  // 3 timed runs + ~10 us per transpose
+        F->wgrad_mode = t_split < t_direct && t_split < tt ? 2 : tt < t_direct ? 1 : 0;
+        if (const char* e = std::getenv("FI_FC_WGRAD")) {  // experiment override: 0 / 1 / 2
+            const int m = std::atoi(e);
+            if (m >= 0 && m <= 2 && (m != 2 || F->split)) F->wgrad_mode = m;
+        }
+    }
     if (rc == FI_OK && std::getenv("FI_VERBOSE"))
-        std::fprintf(stderr, "[fc] wgrad 3 runs: direct %.3f ms, transposed %.3f ms -> %s\n", t_direct, t_trans,
-                     F->wgrad_t ? "transposed" : "direct");
+        std::fprintf(stderr, "[fc] wgrad 3 runs: direct %.3f ms, transposed %.3f ms, split(%d) %.3f ms -> %s\n",
+                     t_direct, t_trans, F->split, t_split,
+                     F->wgrad_mode == 2 ? "split" : F->wgrad_mode == 1 ? "transposed" : "direct");
     if (rc == FI_OK && hipStreamSynchronize(s) != hipSuccess) rc = FI_ERR_HIP;
     if (rc != FI_OK) {
         fc_blaslt_destroy(F);
@@ -214,6 +289,7 @@ void fc_blaslt_destroy(FcBlasLt* F) {
     }
     if (F->ws) (void)hipFree(F->ws);
     if (F->dwT) (void)hipFree(F->dwT);
+    if (F->dwS) (void)hipFree(F->dwS);
     if (F->h) hipblasLtDestroy(F->h);
     delete F;
 }
@@ -235,9 +311,13 @@ int fc_blaslt_dgrad(FcBlasLt* F, const void* dh, const void* w, void* da3, hipSt
 }
 
 int fc_blaslt_wgrad(FcBlasLt* F, const void* a3, const void* dh, float* dw, hipStream_t s) {
-    if (F->wgrad_t) {
+    if (F->wgrad_mode == 1) {
         const int rc = run(F, F->g[3], a3, dh, F->dwT, s);
         return rc ? rc : transpose_f32(F->dwT, 512, 3136, dw, s);
+    }
+    if (F->wgrad_mode == 2) {
+        const int rc = run(F, F->g[4], dh, a3, F->dwS, s);
+        return rc ? rc : reduce_slabs(F->dwS, F->split, (size_t)3136 * 512, dw, s);
     }
     return run(F, F->g[2], dh, a3, dw, s);
 }

@@ -225,3 +225,25 @@ def test_fused_conv21_backward_without_da1_store(monkeypatch):
         gs.append(L.tensor("grads"))
         L.close()
     np.testing.assert_array_equal(gs[0], gs[1])
+
+
+def test_fc_wgrad_split_matches_single_gemm(monkeypatch):
+    """fc weight gradient as a strided batch of row-block GEMMs + a fixed-order sum of the
+    partials (the faster form at the bench shape) against the single GEMM: fcW within fp32
+    summation-order rounding, every other gradient bit-identical. 16,384 frames, 8 blocks."""
+    T, B = 3, 4096
+    fcw = slice(77984, 77984 + 3136 * 512)
+    gs = {}
+    monkeypatch.setenv("FI_FC_SPLIT", "8")
+    for mode in ("0", "2"):
+        monkeypatch.setenv("FI_FC_WGRAD", mode)
+        L = mk(T=T, B=B, seed=6)
+        L.synth(seed=23)
+        L.step_resident()
+        gs[mode] = L.tensor("grads")
+        L.close()
+    a, b = gs["2"], gs["0"]
+    assert np.isfinite(a).all()
+    rel(a[fcw], b[fcw], "fcW", l2=1e-5, mx=1e-4)
+    np.testing.assert_array_equal(a[:fcw.start], b[:fcw.start])
+    np.testing.assert_array_equal(a[fcw.stop:], b[fcw.stop:])
