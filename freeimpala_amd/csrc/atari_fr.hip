@@ -72,12 +72,13 @@ static void st_report(const char*) {}
 
 #ifdef FI_PHASES  // timing experiment: per-phase clock sums of waves 0 and 4, per workgroup
 __device__ unsigned long long fi_phases[1024 * 16];
-#define PH_DECL unsigned long long ph_[6] = {0, 0, 0, 0, 0, 0}, pt_ = __builtin_amdgcn_s_memtime(); int pn_ = 0;
+#define PH_DECL unsigned long long ph_[6] = {0, 0, 0, 0, 0, 0}, pt_ = __builtin_amdgcn_s_memtime(), rt0_ = __builtin_amdgcn_s_memrealtime(), ct0_ = pt_; int pn_ = 0;
 #define PH(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); ph_[k] += t_ - pt_; pt_ = t_; } while (0)
 #define PH_ITER() (++pn_)
 #define PH_FLUSH() do { const int w_ = wave_id(); if ((threadIdx.x & 63) == 0 && (w_ == 0 || w_ == 4) && blockIdx.x < 1024) { \
     for (int k_ = 0; k_ < 6; ++k_) fi_phases[blockIdx.x * 16 + (w_ ? 8 : 0) + k_] = ph_[k_]; \
-    fi_phases[blockIdx.x * 16 + (w_ ? 8 : 0) + 7] = pn_; } } while (0)
+    fi_phases[blockIdx.x * 16 + (w_ ? 8 : 0) + 7] = pn_; \
+    fi_phases[blockIdx.x * 16 + (w_ ? 8 : 0) + 6] = ((__builtin_amdgcn_s_memtime() - ct0_) << 20) / max(1ull, __builtin_amdgcn_s_memrealtime() - rt0_); } } while (0)
 #include <cstdio>
 #include <vector>
 static void ph_report(const char* name, int grid) {
@@ -97,9 +98,12 @@ static void ph_report(const char* name, int grid) {
             for (int k = 0; k < 6; ++k) sum[k] += (double)h[b * 16 + 8 * r + k];
             n += (double)h[b * 16 + 8 * r + 7];
         }
+        double mhz = 0;  // shader clocks per 100 MHz real-time tick (s_memrealtime), mean over workgroups
+        int nb = 0;
+        for (int b = 0; b < grid && b < 1024; ++b, ++nb) mhz += (double)h[b * 16 + 8 * r + 6] / (1 << 20) * 100.0;
         std::fprintf(stderr, "[phases %s wave %d] clk/frame:", name, 4 * r);
         for (int k = 0; k < 6; ++k) std::fprintf(stderr, " %.0f", sum[k] / (n > 0 ? n : 1));
-        std::fprintf(stderr, "\n");
+        std::fprintf(stderr, "  clock %.0f MHz\n", nb ? mhz / nb : 0.0);
     }
 }
 #else
@@ -1509,18 +1513,31 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                     *(bf16x8*)(IMG + c1::PLANE + 16 * u) = hi;
                 }
             }
+#if !defined(FI_EXP_NORAW) && !defined(FI_C21_RAW_LATE)  // NORAW: timing experiment, raw frame loaded once (wrong results)
+            // raw(it + 1) goes out now, while this wave waits at B2 for the data-gradient
+            // waves: in phase 2 its issue would queue behind the DMA (several thousand clocks
+            // of issue stall per frame with both there)
+            if (it + 1 < nmine) {
+                load_raw(it + 1);
+                issued += c21::NRAW_A;
+            }
+#endif
             PH(3);
             lds_barrier();  // B2: D and the image complete; da2 image and a1 slot it&1 consumed
             PH(1);
+#ifndef FI_EXP_NOISSUE2  // timing experiment: no DMA after frame 0 (wrong results)
             if (it + 1 < nmine) {
                 issued += issue_dy(it + 1);
                 m_dy = issued;
             }
             if (it + 2 < nmine) issued += issue_ax(it + 2, it & 1);
+#endif
+#ifdef FI_C21_RAW_LATE  // A/B: raw(it + 1) loaded after the phase-2 DMA issue
             if (it + 1 < nmine) {
                 load_raw(it + 1);
                 issued += c21::NRAW_A;
             }
+#endif
             PH(4);
             PH_ITER();
         }
