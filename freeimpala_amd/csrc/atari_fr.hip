@@ -1319,9 +1319,11 @@ constexpr int LDS = O_TAB + (c2::XB + c2::DYB) / 16 * 4;  // 160,256
 #endif
 constexpr int NRAW_A = FI_C21_NRAW_A;  // 16-B raw-frame units per lane converted by waves 0-3
 constexpr int NRAW_B = 7 - NRAW_A;     // ... by waves 4-7 (the rest of the 1,764)
+
 static_assert(256 * (NRAW_A + NRAW_B) >= c1::FRAME_LOADS, "raw-frame split");
 }  // namespace c21
 
+template <bool KEEP_DA1>  // KEEP_DA1: also store da1 to HBM (parity checks); no branch in the hot loop
 __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict__ a1,
                                                         const __bf16* __restrict__ da2,
                                                         const __bf16* __restrict__ w2d,  // [4][32][256]
@@ -1595,7 +1597,7 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
             PH(1);
             {  // conv2 data gradient of class (ty, tx) -> D (and da1_out)
                 const char* X = smem + c21::O_AX + (it & 1) * c21::AXB;
-                u32x4* dst = da1_out ? (u32x4*)(da1_out + (size_t)f * 12800) : nullptr;
+                u32x4* dst = KEEP_DA1 ? (u32x4*)(da1_out + (size_t)f * 12800) : nullptr;
                 // step st = (pixel tile pt, k-step ks): dY fragment read PD steps ahead
                 auto frag = [&](int st) {
                     const int pt = st >> 3, ks = st & 7, tap = ks >> 1, kty = tap >> 1, ktx = tap & 1;
@@ -1612,8 +1614,31 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                 auto mask_of = [&](int pt) {
                     return *(const s16x8*)(X + 64 * (100 * wr + min(pt * 16 + si, 99)) + 16 * g);
                 };
+                // tile pt's epilogue: mask by (a1 > 0), into D (and da1_out), conv1 bias partials
+                auto epilogue = [&](int pt, const f32x4& e0, const f32x4& e1, const s16x8& m) {
+                    const int ri = pt * 16 + si;
+                    if (pt < 6 || ri < 100) {
+                        const int iyq = ri / 10, ixq = ri - 10 * iyq;
+                        const int pix = (2 * iyq + ty) * 20 + 2 * ixq + tx;
+                        bf16x8 o;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            o[r] = m[r] > 0 ? (__bf16)e0[r] : (__bf16)0.f;
+                            o[4 + r] = m[4 + r] > 0 ? (__bf16)e1[r] : (__bf16)0.f;
+                        }
+                        const u32x4 ov = __builtin_bit_cast(u32x4, o);
+#ifndef FI_EXP_NODW  // timing experiment: no da1 tile writes (wrong results)
+                        *(u32x4*)(D + dsw(pix, g)) = ov;
+#endif
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) bs8[j] += (float)o[j];
+                        if constexpr (KEEP_DA1) FI_ST16(ov, dst + 4 * pix + g);
+                    }
+                };
                 s16x8 mk = mask_of(0);
                 f32x4 ac0 = f32x4{}, ac1 = f32x4{};
+                // (a software-pipelined form -- tile pt-1's epilogue spread over tile pt's MFMAs --
+                // measured slower: 6.2k -> 6.8k clocks per frame for this phase)
 #pragma unroll
                 for (int st = 0; st < NSTEP; ++st) {
                     const int pt = st >> 3, ks = st & 7;
@@ -1623,27 +1648,10 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                     ac1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[1][ks], b, ac1, 0, 0, 0);
                     __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
                     if (st + PD < NSTEP) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                    if (ks == 7) {  // tile pt done: mask by (a1 > 0), into D
+                    if (ks == 7) {
                         const s16x8 m = mk;
                         if (pt + 1 < 7) mk = mask_of(pt + 1);
-                        const int ri = pt * 16 + si;
-                        if (pt < 6 || ri < 100) {
-                            const int iyq = ri / 10, ixq = ri - 10 * iyq;
-                            const int pix = (2 * iyq + ty) * 20 + 2 * ixq + tx;
-                            bf16x8 o;
-#pragma unroll
-                            for (int r = 0; r < 4; ++r) {
-                                o[r] = m[r] > 0 ? (__bf16)ac0[r] : (__bf16)0.f;
-                                o[4 + r] = m[4 + r] > 0 ? (__bf16)ac1[r] : (__bf16)0.f;
-                            }
-                            const u32x4 ov = __builtin_bit_cast(u32x4, o);
-#ifndef FI_EXP_NODW  // timing experiment: no da1 tile writes (wrong results)
-                            *(u32x4*)(D + dsw(pix, g)) = ov;
-#endif
-#pragma unroll
-                            for (int j = 0; j < 8; ++j) bs8[j] += (float)o[j];
-                            if (dst) FI_ST16(ov, dst + 4 * pix + g);
-                        }
+                        epilogue(pt, ac0, ac1, m);
                         ac0 = f32x4{};
                         ac1 = f32x4{};
                     }
@@ -1693,7 +1701,11 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
 int conv21_bwd_fr_launch(const __bf16* a1, const __bf16* da2, const __bf16* w2d, const uint8_t* frames,
                          __bf16* da1_out, float* slab2, float* cs2, float* slab1, float* cs1, int nframes,
                          int grid, hipStream_t s) {
-    hipLaunchKernelGGL(conv21_bwd_fr, dim3(grid), dim3(512), 0, s, a1, da2, w2d, frames, da1_out, slab2, cs2,
+    if (da1_out)
+        hipLaunchKernelGGL(conv21_bwd_fr<true>, dim3(grid), dim3(512), 0, s, a1, da2, w2d, frames, da1_out, slab2,
+                           cs2, slab1, cs1, nframes);
+    else
+        hipLaunchKernelGGL(conv21_bwd_fr<false>, dim3(grid), dim3(512), 0, s, a1, da2, w2d, frames, da1_out, slab2, cs2,
                        slab1, cs1, nframes);
     FI_HIP_CHECK(hipGetLastError());
     ph_report("conv21_bwd", grid);
