@@ -148,7 +148,15 @@ def main():
 
     ws, rank, local = dist_env()
     N = max(ws, 1)
-    import torch
+    # the learner library first: it then binds the image's ROCm 7.2 runtime, hipBLASLt and RCCL
+    # (what it is built against, and what the tests and smoke() load); imported first, torch's
+    # bundled ROCm 7.0 copies would take those sonames. torch is only the gloo launcher here
+    # and never touches the GPU.
+    if os.environ.get("FI_BENCH_TORCH_FIRST"):  # A/B only: torch's bundled ROCm libraries
+        import torch  # noqa: F401
+    from freeimpala_amd import _abi
+    _abi.lib()
+    import torch  # noqa: F401,F811
     import torch.distributed as dist
     if ws > 1:
         dist.init_process_group("gloo", rank=rank, world_size=ws)

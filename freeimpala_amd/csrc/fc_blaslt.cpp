@@ -10,14 +10,16 @@
 //   wgrad    dW[3136][512] = a3^T dh  (fp32 out, straight into the gradient blob)
 // All row-major; hipBLASLt is column-major, so each call computes the transposed product.
 // W is the bf16 copy of the fp32 master in the oracle's [3136][512] order.
-// Algorithms: the heuristic's top 64 candidates are timed once at creation (16 missed a dgrad
-// kernel 17 % faster), on operands filled
+// Algorithms: the heuristic's top 64 candidates (plus, at the bench shape, the fastest few of an
+// exhaustive sweep, kSweepBest) are timed once at creation (16 missed a dgrad kernel 17 % faster),
+// on operands filled
 // with hashed bf16 values (the chip's clock under load depends on the data: candidates timed
 // on zero-filled buffers ranked differently from the step), and the fastest kept. The choice is
 // cached per GEMM shape for the life of the process, so every learner handle of one process
 // runs the same algorithms and produces bit-identical results on identical inputs.
 #include <hip/hip_runtime.h>
 #include <hipblaslt/hipblaslt.h>
+#include <hipblaslt/hipblaslt-ext.hpp>
 
 #include <cstdio>
 #include <cstdlib>
@@ -25,6 +27,7 @@
 #include <mutex>
 #include <string>
 #include <tuple>
+#include <vector>
 
 #include "fc_blaslt.h"
 #include "fi_common.h"
@@ -58,14 +61,33 @@ static std::string blt_err(const char* what, int st) { return std::string(what) 
         if (st_ != 0) { set_error(blt_err(#x, st_)); return FI_ERR_HIP; } \
     } while (0)
 
-// shape -> index of the timed winner in the (deterministic) heuristic list
+// shape -> hipBLASLt solution index of the timed winner (+ its time)
 using GemmKey = std::tuple<int, int, int, bool, bool, int, int, int>;
 #ifndef FI_BLT_CAND
 #define FI_BLT_CAND 64
 #endif
 constexpr int kCand = FI_BLT_CAND;  // heuristic candidates timed at creation
 static std::mutex g_algo_mu;
-static std::map<GemmKey, std::pair<int, float>> g_algo_choice;  // -> (index, ms of 3 runs)
+static std::map<GemmKey, std::pair<int, float>> g_algo_choice;  // -> (solution index, ms of 3 runs)
+static std::map<int, int> g_wgrad_form;  // rows -> wgrad form (0 direct, 1 transposed, 2 + S split)
+
+static void destroy_gemm(FcGemm& G) {
+    if (G.la) hipblasLtMatrixLayoutDestroy(G.la);
+    if (G.lb) hipblasLtMatrixLayoutDestroy(G.lb);
+    if (G.ld) hipblasLtMatrixLayoutDestroy(G.ld);
+    if (G.desc) hipblasLtMatmulDescDestroy(G.desc);
+    G = FcGemm{};
+}
+
+// Extra candidates for the bench shape (R = 101 * 4096 rows), from an exhaustive sweep of every
+// solution hipBLASLt 1.x of this image supports (scripts/blaslt_all.cpp: 1,242 forward and 2,050
+// data-gradient solutions; the fastest ones are not in the heuristic's top 64). Solution indices
+// are library-version specific: any that this library does not know or that does not support the
+// problem is skipped, so the heuristic list alone remains the fallback.
+static const std::map<std::tuple<int, int, int, bool, bool, int>, std::vector<int>> kSweepBest = {
+    {{512, 101 * 4096, 3136, false, false, 1}, {436555, 437491, 436281, 436558, 436613, 436554}},
+    {{3136, 101 * 4096, 512, true, false, 1}, {439401, 439365, 440236, 438309, 439398, 440239}},
+};
 
 static int make_gemm(FcBlasLt* F, FcGemm& G, int m, int n, int k, bool ta, bool tb, hipDataType dt_d,
                      hipblasLtEpilogue_t epi, const void* A, const void* B, void* D, hipStream_t s,
@@ -78,6 +100,8 @@ static int make_gemm(FcBlasLt* F, FcGemm& G, int m, int n, int k, bool ta, bool 
     if (epi == HIPBLASLT_EPILOGUE_RELU_BIAS) {
         const hipDataType bt = HIP_R_32F;
         BLT(hipblasLtMatmulDescSetAttribute(G.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt)));
+        const void* bias = D;  // any readable device buffer of >= m floats (timing only; set per call)
+        BLT(hipblasLtMatmulDescSetAttribute(G.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias)));
     }
     BLT(hipblasLtMatrixLayoutCreate(&G.la, HIP_R_16BF, ta ? k : m, ta ? m : k, ta ? k : m));
     BLT(hipblasLtMatrixLayoutCreate(&G.lb, HIP_R_16BF, tb ? n : k, tb ? k : n, tb ? n : k));
@@ -94,50 +118,79 @@ static int make_gemm(FcBlasLt* F, FcGemm& G, int m, int n, int k, bool ta, bool 
     BLT(hipblasLtMatmulPreferenceCreate(&pref));
     BLT(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &F->wsb,
                                               sizeof(F->wsb)));
-    hipblasLtMatmulHeuristicResult_t res[kCand];
+    std::vector<hipblasLtMatmulHeuristicResult_t> cands(kCand);
     int got = 0;
-    const int st = (int)hipblasLtMatmulAlgoGetHeuristic(F->h, G.desc, G.la, G.lb, G.ld, G.ld, pref, kCand, res, &got);
+    const int st = (int)hipblasLtMatmulAlgoGetHeuristic(F->h, G.desc, G.la, G.lb, G.ld, G.ld, pref, kCand,
+                                                        cands.data(), &got);
     hipblasLtMatmulPreferenceDestroy(pref);
     if (st != 0 || got == 0) {
         set_error("hipBLASLt: no algorithm for the fc GEMM (m=" + std::to_string(m) + " n=" + std::to_string(n) +
                   " k=" + std::to_string(k) + ")");
         return FI_ERR_UNSUPPORTED;
     }
+    cands.resize(got);
+    const float alpha = 1.f, beta = 0.f;
+    // solutions by index (the sweep table, or a cached winner): kept only if this library knows
+    // them and they support this problem within the workspace
+    auto add_by_index = [&](std::vector<int> idx) {
+        std::vector<hipblasLtMatmulHeuristicResult_t> ex;
+        const int rc = idx.empty() ? -1 : (int)hipblaslt_ext::getAlgosFromIndex(F->h, idx, ex);
+        if (std::getenv("FI_VERBOSE"))
+            std::fprintf(stderr, "[fc] %zu solutions by index: rc %d, %zu returned\n", idx.size(), rc, ex.size());
+        if (rc != 0) return;
+        for (auto& r : ex) {
+            size_t need = 0;
+            const int sup = (int)hipblaslt_ext::matmulIsAlgoSupported(F->h, G.desc, &alpha, G.la, G.lb, &beta, G.ld,
+                                                                      G.ld, r.algo, need);
+            if (std::getenv("FI_VERBOSE"))
+                std::fprintf(stderr, "[fc]   solution %d: supported rc %d, workspace %zu\n",
+                             hipblaslt_ext::getIndexFromAlgo(r.algo), sup, need);
+            if (sup == 0 && need <= F->wsb) cands.push_back(r);
+        }
+    };
+    auto find_index = [&](int idx) -> int {
+        for (size_t a = 0; a < cands.size(); ++a)
+            if (hipblaslt_ext::getIndexFromAlgo(cands[a].algo) == idx) return (int)a;
+        return -1;
+    };
     const GemmKey key{m, n, k, ta, tb, (int)dt_d, (int)epi, batch};
     {
         std::lock_guard<std::mutex> lk(g_algo_mu);
         auto it = g_algo_choice.find(key);
-        if (it != g_algo_choice.end() && it->second.first < got) {
-            G.algo = res[it->second.first].algo;
-            if (best_ms) *best_ms = it->second.second;
-            return FI_OK;
+        if (it != g_algo_choice.end()) {  // same solution as every other handle of this process
+            int a = find_index(it->second.first);
+            if (a < 0) {
+                add_by_index({it->second.first});
+                a = find_index(it->second.first);
+            }
+            if (a >= 0) {
+                G.algo = cands[a].algo;
+                if (best_ms) *best_ms = it->second.second;
+                return FI_OK;
+            }
         }
     }
-    // time the candidates once (the tensors hold garbage at creation; only speed matters)
-    const float alpha = 1.f, beta = 0.f;
+    auto tuned = kSweepBest.find({m, n, k, ta, tb, batch});
+    if (tuned != kSweepBest.end() && !std::getenv("FI_BLT_NO_SWEEP")) add_by_index(tuned->second);
+    // time the candidates once (the tensors hold hashed data at creation; only speed matters)
     hipEvent_t e0, e1;
     FI_HIP_CHECK(hipEventCreate(&e0));
     FI_HIP_CHECK(hipEventCreate(&e1));
     float best = 1e30f;
     int bi = 0;
-    const void* bias = nullptr;
-    for (int a = 0; a < got; ++a) {
-        if (epi == HIPBLASLT_EPILOGUE_RELU_BIAS) {
-            bias = D;  // any readable device buffer of >= m floats
-            BLT(hipblasLtMatmulDescSetAttribute(G.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias)));
-        }
-        if (hipblasLtMatmul(F->h, G.desc, &alpha, A, G.la, B, G.lb, &beta, D, G.ld, D, G.ld, &res[a].algo, F->ws,
+    for (size_t a = 0; a < cands.size(); ++a) {
+        if (hipblasLtMatmul(F->h, G.desc, &alpha, A, G.la, B, G.lb, &beta, D, G.ld, D, G.ld, &cands[a].algo, F->ws,
                             F->wsb, s) != 0)
             continue;
         FI_HIP_CHECK(hipEventRecord(e0, s));
         for (int i = 0; i < 3; ++i)
-            BLT(hipblasLtMatmul(F->h, G.desc, &alpha, A, G.la, B, G.lb, &beta, D, G.ld, D, G.ld, &res[a].algo,
+            BLT(hipblasLtMatmul(F->h, G.desc, &alpha, A, G.la, B, G.lb, &beta, D, G.ld, D, G.ld, &cands[a].algo,
                                 F->ws, F->wsb, s));
         FI_HIP_CHECK(hipEventRecord(e1, s));
         FI_HIP_CHECK(hipEventSynchronize(e1));
         float ms = 0.f;
         FI_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
-        if (ms < best) { best = ms; bi = a; }
+        if (ms < best) { best = ms; bi = (int)a; }
     }
     hipEventDestroy(e0);
     hipEventDestroy(e1);
@@ -145,9 +198,15 @@ static int make_gemm(FcBlasLt* F, FcGemm& G, int m, int n, int k, bool ta, bool 
         set_error("hipBLASLt: every fc GEMM candidate failed to launch");
         return FI_ERR_UNSUPPORTED;
     }
+    if (std::getenv("FI_VERBOSE"))
+        std::fprintf(stderr, "[fc] gemm m=%d n=%d k=%d batch=%d: %zu candidates (%d heuristic), best #%d %s %.3f ms/3\n",
+                     m, n, k, batch, cands.size(), got, bi, bi >= got ? "(sweep)" : "(heuristic)", best);
     std::lock_guard<std::mutex> lk(g_algo_mu);
-    g_algo_choice.emplace(key, std::make_pair(bi, best));  // first timing wins for the whole process
-    G.algo = res[g_algo_choice[key].first].algo;
+    // first timing wins for the whole process
+    g_algo_choice.emplace(key, std::make_pair(hipblaslt_ext::getIndexFromAlgo(cands[bi].algo), best));
+    const int want = g_algo_choice[key].first;
+    int a = find_index(want);
+    G.algo = cands[a >= 0 ? a : bi].algo;
     if (best_ms) *best_ms = g_algo_choice[key].second;
     return FI_OK;
 }
@@ -170,21 +229,6 @@ static int transpose_f32(const float* src, int R, int C, float* dst, hipStream_t
     hipLaunchKernelGGL(transpose_f32_kernel, dim3((C + 31) / 32, (R + 31) / 32), dim3(256), 0, s, src, R, C, dst);
     FI_HIP_CHECK(hipGetLastError());
     return FI_OK;
-}
-
-static int time_reduce(const float* slab, int S, size_t count, float* out, hipStream_t s, float* ms) {
-    hipEvent_t e0, e1;
-    FI_HIP_CHECK(hipEventCreate(&e0));
-    FI_HIP_CHECK(hipEventCreate(&e1));
-    int rc = FI_OK;
-    if (hipEventRecord(e0, s) != hipSuccess) rc = FI_ERR_HIP;
-    for (int i = 0; i < 3 && rc == FI_OK; ++i) rc = reduce_slabs(slab, S, count, out, s);
-    if (rc == FI_OK && (hipEventRecord(e1, s) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
-                        hipEventElapsedTime(ms, e0, e1) != hipSuccess))
-        rc = FI_ERR_HIP;
-    hipEventDestroy(e0);
-    hipEventDestroy(e1);
-    return rc;
 }
 
 FcBlasLt* fc_blaslt_create(int rows, const void* a3, const void* w, const void* dh, void* h, void* da3,
@@ -210,67 +254,107 @@ FcBlasLt* fc_blaslt_create(int rows, const void* a3, const void* w, const void* 
     // column-major views of the row-major products (see the header comment)
     if (rc == FI_OK) rc = make_gemm(F, F->g[0], N, rows, K, false, false, HIP_R_16BF, HIPBLASLT_EPILOGUE_RELU_BIAS, w, a3, h, s);
     if (rc == FI_OK) rc = make_gemm(F, F->g[1], K, rows, N, true, false, HIP_R_16BF, HIPBLASLT_EPILOGUE_DEFAULT, w, dh, da3, s);
-    // wgrad in both orientations: dW (column-major N x K) directly, or dW^T (K x N) + a transpose
-    float t_direct = 0.f, t_trans = 0.f;
-    if (rc == FI_OK) rc = make_gemm(F, F->g[2], N, K, rows, false, true, HIP_R_32F, HIPBLASLT_EPILOGUE_DEFAULT, dh, a3, dw, s, &t_direct);
+    // wgrad forms: dW (column-major N x K) directly, dW^T (K x N) + a transpose, or S row blocks
+    // as one strided-batched GEMM (S partial dW) summed by reduce_slabs in a fixed order
+    // (S from FI_FC_SPLIT, or each of 8 / 16 / 32 / 64 that divides the rows)
+    if (rc == FI_OK) rc = make_gemm(F, F->g[2], N, K, rows, false, true, HIP_R_32F, HIPBLASLT_EPILOGUE_DEFAULT, dh, a3, dw, s);
     if (rc == FI_OK && hipMalloc((void**)&F->dwT, (size_t)K * N * sizeof(float)) != hipSuccess) {
         set_error("fc: dW^T scratch allocation failed");
         rc = FI_ERR_OOM;
     }
-    if (rc == FI_OK) rc = make_gemm(F, F->g[3], K, N, rows, false, true, HIP_R_32F, HIPBLASLT_EPILOGUE_DEFAULT, a3, dh, F->dwT, s, &t_trans);
-    // split wgrad: S row blocks as one strided-batched GEMM (S partial dW), summed by
-    // reduce_slabs in a fixed order; S from FI_FC_SPLIT, or the fastest of 8 / 16 / 32 / 64
-    float t_split = 1e30f;
+    if (rc == FI_OK) rc = make_gemm(F, F->g[3], K, N, rows, false, true, HIP_R_32F, HIPBLASLT_EPILOGUE_DEFAULT, a3, dh, F->dwT, s);
+    struct SplitForm {
+        int S;
+        FcGemm G;
+        float* slab;
+    };
+    std::vector<SplitForm> splits;
     if (rc == FI_OK) {
         const char* e = std::getenv("FI_FC_SPLIT");
         const int fixed = e ? std::atoi(e) : 0;
         for (int S : {8, 16, 32, 64}) {
-            if (fixed > 0 && S != fixed) continue;
-            if (rows % S || rows / S < 2048) continue;
-            float* slab = nullptr;
-            if (hipMalloc((void**)&slab, (size_t)S * K * N * sizeof(float)) != hipSuccess) break;
-            FcGemm G;
-            float t = 0.f;
-            int r2 = make_gemm(F, G, N, K, rows / S, false, true, HIP_R_32F, HIPBLASLT_EPILOGUE_DEFAULT, dh, a3,
-                               slab, s, &t, S);
-            float tr = 0.f;  // + the partial sum: 3 runs, as the GEMM timing
-            if (r2 == FI_OK) r2 = time_reduce(slab, S, (size_t)K * N, dw, s, &tr);
-            t += tr;
-            if (std::getenv("FI_VERBOSE"))
-                std::fprintf(stderr, "[fc] wgrad split %d, 3 runs incl. sum: %.3f ms\n", S, t);
-            if (r2 == FI_OK && t < t_split) {
-                t_split = t;
-                for (FcGemm* X : {&F->g[4]}) {
-                    if (X->la) hipblasLtMatrixLayoutDestroy(X->la);
-                    if (X->lb) hipblasLtMatrixLayoutDestroy(X->lb);
-                    if (X->ld) hipblasLtMatrixLayoutDestroy(X->ld);
-                    if (X->desc) hipblasLtMatmulDescDestroy(X->desc);
-                }
-                F->g[4] = G;
-                if (F->dwS) (void)hipFree(F->dwS);
-                F->dwS = slab;
-                F->split = S;
-            } else {
-                if (G.la) hipblasLtMatrixLayoutDestroy(G.la);
-                if (G.lb) hipblasLtMatrixLayoutDestroy(G.lb);
-                if (G.ld) hipblasLtMatrixLayoutDestroy(G.ld);
-                if (G.desc) hipblasLtMatmulDescDestroy(G.desc);
-                (void)hipFree(slab);
+            if ((fixed > 0 && S != fixed) || rows % S || rows / S < 2048) continue;
+            SplitForm sf{S, FcGemm{}, nullptr};
+            if (hipMalloc((void**)&sf.slab, (size_t)S * K * N * sizeof(float)) != hipSuccess) break;
+            if (make_gemm(F, sf.G, N, K, rows / S, false, true, HIP_R_32F, HIPBLASLT_EPILOGUE_DEFAULT, dh, a3, sf.slab,
+                          s, nullptr, S) == FI_OK)
+                splits.push_back(sf);
+            else
+                destroy_gemm(sf.G), (void)hipFree(sf.slab);
+        }
+    }
+    // form 0 direct, 1 transposed, 2 + i split i: the process-wide choice for this row count
+    // (every handle of the process then computes bit-identical gradients), else a tournament:
+    // 2 rounds x 4 timed runs of each complete form (GEMM + transpose / partial sum), min kept
+    int form = -1;
+    if (rc == FI_OK) {
+        std::lock_guard<std::mutex> lk(g_algo_mu);
+        auto it = g_wgrad_form.find(rows);
+        if (it != g_wgrad_form.end()) {
+            if (it->second < 2) form = it->second;
+            for (size_t i = 0; i < splits.size(); ++i)
+                if (it->second == 2 + splits[i].S) form = 2 + (int)i;
+        }
+    }
+    auto run_form = [&](int f) -> int {
+        const float alpha = 1.f, beta = 0.f;
+        if (f == 0) { BLT(hipblasLtMatmul(F->h, F->g[2].desc, &alpha, dh, F->g[2].la, a3, F->g[2].lb, &beta, dw, F->g[2].ld, dw, F->g[2].ld, &F->g[2].algo, F->ws, F->wsb, s)); return FI_OK; }
+        if (f == 1) {
+            BLT(hipblasLtMatmul(F->h, F->g[3].desc, &alpha, a3, F->g[3].la, dh, F->g[3].lb, &beta, F->dwT, F->g[3].ld, F->dwT, F->g[3].ld, &F->g[3].algo, F->ws, F->wsb, s));
+            return transpose_f32(F->dwT, 512, 3136, dw, s);
+        }
+        SplitForm& sf = splits[f - 2];
+        BLT(hipblasLtMatmul(F->h, sf.G.desc, &alpha, dh, sf.G.la, a3, sf.G.lb, &beta, sf.slab, sf.G.ld, sf.slab, sf.G.ld, &sf.G.algo, F->ws, F->wsb, s));
+        return reduce_slabs(sf.slab, sf.S, (size_t)K * N, dw, s);
+    };
+    if (rc == FI_OK && form < 0) {
+        const int nf = 2 + (int)splits.size();
+        std::vector<float> best(nf, 1e30f);
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) rc = FI_ERR_HIP;
+        for (int round = 0; round < 2 && rc == FI_OK; ++round)
+            for (int f = 0; f < nf && rc == FI_OK; ++f) {
+                rc = run_form(f);  // warm
+                if (rc == FI_OK && hipEventRecord(e0, s) != hipSuccess) rc = FI_ERR_HIP;
+                for (int i = 0; i < 4 && rc == FI_OK; ++i) rc = run_form(f);
+                float ms = 0.f;
+                if (rc == FI_OK && (hipEventRecord(e1, s) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+                                    hipEventElapsedTime(&ms, e0, e1) != hipSuccess))
+                    rc = FI_ERR_HIP;
+                if (rc == FI_OK) best[f] = std::min(best[f], ms / 4);
             }
+        if (e0) hipEventDestroy(e0);
+        if (e1) hipEventDestroy(e1);
+        if (rc == FI_OK) {
+            form = 0;
+            for (int f = 1; f < nf; ++f)
+                if (best[f] < best[form]) form = f;
+            if (std::getenv("FI_VERBOSE")) {
+                std::fprintf(stderr, "[fc] wgrad forms (ms/run): direct %.3f, transposed %.3f", best[0], best[1]);
+                for (size_t i = 0; i < splits.size(); ++i) std::fprintf(stderr, ", split %d %.3f", splits[i].S, best[2 + i]);
+                std::fprintf(stderr, " -> form %d\n", form);
+            }
+            std::lock_guard<std::mutex> lk(g_algo_mu);
+            g_wgrad_form.emplace(rows, form < 2 ? form : 2 + splits[form - 2].S);  // first timing wins
         }
     }
     if (rc == FI_OK) {
-        const float tt = t_trans + 0.03f;  // 3 timed runs + ~10 us per transpose
-        F->wgrad_mode = t_split < t_direct && t_split < tt ? 2 : tt < t_direct ? 1 : 0;
-        if (const char* e = std::getenv("FI_FC_WGRAD")) {  // experiment override: 0 / 1 / 2
+        if (const char* e = std::getenv("FI_FC_WGRAD")) {  // experiment override: 0 / 1 / 2 (first split)
             const int m = std::atoi(e);
-            if (m >= 0 && m <= 2 && (m != 2 || F->split)) F->wgrad_mode = m;
+            if (m >= 0 && m <= 2 && (m != 2 || !splits.empty())) form = m;
+        }
+        F->wgrad_mode = form < 2 ? form : 2;
+    }
+    for (size_t i = 0; i < splits.size(); ++i) {  // keep the chosen split form only
+        if (rc == FI_OK && form == 2 + (int)i) {
+            F->g[4] = splits[i].G;
+            F->dwS = splits[i].slab;
+            F->split = splits[i].S;
+        } else {
+            destroy_gemm(splits[i].G);
+            (void)hipFree(splits[i].slab);
         }
     }
-    if (rc == FI_OK && std::getenv("FI_VERBOSE"))
-        std::fprintf(stderr, "[fc] wgrad 3 runs: direct %.3f ms, transposed %.3f ms, split(%d) %.3f ms -> %s\n",
-                     t_direct, t_trans, F->split, t_split,
-                     F->wgrad_mode == 2 ? "split" : F->wgrad_mode == 1 ? "transposed" : "direct");
     if (rc == FI_OK && hipStreamSynchronize(s) != hipSuccess) rc = FI_ERR_HIP;
     if (rc != FI_OK) {
         fc_blaslt_destroy(F);
@@ -281,12 +365,7 @@ FcBlasLt* fc_blaslt_create(int rows, const void* a3, const void* w, const void* 
 
 void fc_blaslt_destroy(FcBlasLt* F) {
     if (!F) return;
-    for (auto& G : F->g) {
-        if (G.la) hipblasLtMatrixLayoutDestroy(G.la);
-        if (G.lb) hipblasLtMatrixLayoutDestroy(G.lb);
-        if (G.ld) hipblasLtMatrixLayoutDestroy(G.ld);
-        if (G.desc) hipblasLtMatmulDescDestroy(G.desc);
-    }
+    for (auto& G : F->g) destroy_gemm(G);
     if (F->ws) (void)hipFree(F->ws);
     if (F->dwT) (void)hipFree(F->dwT);
     if (F->dwS) (void)hipFree(F->dwS);

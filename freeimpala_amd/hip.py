@@ -16,7 +16,9 @@ H2D, D2H, D2D = 1, 2, 3
 def hip():
     global _hip
     if _hip is None:
-        L = C.CDLL("libamdhip64.so")
+        # by soname: the runtime libfi_learner.so is bound to (the image's, or torch's copy
+        # when torch was imported first), never a second HIP runtime in the process
+        L = C.CDLL("libamdhip64.so.7")
         L.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
         L.hipFree.argtypes = [C.c_void_p]
         L.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
