@@ -896,7 +896,9 @@ extern "C" int fi_learner_attach_comm(fi_learner* l, const void* uid, size_t byt
         ncclCommDestroy(l->comm);
         l->comm = nullptr;
     }
-    if (nranks == 1) return FI_OK;
+    // one rank: no communicator (the sum over one rank is the identity), unless FI_COMM_SINGLE
+    // asks for one -- the tests use it to run the in-step all-reduce path on a single GPU
+    if (nranks == 1 && !std::getenv("FI_COMM_SINGLE")) return FI_OK;
     ncclUniqueId id;
     std::memcpy(&id, uid, sizeof(id));
     ncclResult_t r = ncclCommInitRank(&l->comm, nranks, id, rank);

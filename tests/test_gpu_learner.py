@@ -246,6 +246,27 @@ def test_staged_steps_match_entry_steps(orc):
     assert s1["total_loss"] == s2["total_loss"] and s1["version"] == s2["version"] == 5
 
 
+def test_rccl_one_rank_allreduce_step_matches(monkeypatch):
+    """The data-parallel path on one GPU: a handle attached to a one-rank RCCL communicator
+    (FI_COMM_SINGLE) runs the in-step ncclAllReduce(sum) of the flat gradient on its stream;
+    a one-rank sum is the identity, so its parameters after three Adam steps equal those of a
+    handle without a communicator, bit for bit. Covers unique id / attach / all-reduce /
+    teardown; N > 1 needs several GPUs (RCCL refuses two ranks on one device)."""
+    from freeimpala_amd.learner import DeviceLearner
+    monkeypatch.setenv("FI_COMM_SINGLE", "1")
+    L1, L2 = mk(T=4, B=32, seed=5, optimizer="adam"), mk(T=4, B=32, seed=5, optimizer="adam")
+    L2.attach_comm(DeviceLearner.comm_unique_id(), 0, 1)
+    s = {}
+    for i, L in enumerate((L1, L2)):
+        L.synth(seed=12)
+        for _ in range(3):
+            s[i] = L.step_resident()
+    np.testing.assert_array_equal(L1.get_params(), L2.get_params())
+    assert s[0]["total_loss"] == s[1]["total_loss"]
+    L1.close()
+    L2.close()
+
+
 def test_state_checkpoint_resume_is_bit_exact():
     """save_state after one step, load it into a fresh learner, step both on the same batch:
     identical parameters and Adam moments (optimizer state restored, not just weights)."""
