@@ -41,7 +41,7 @@ def test_atari_synth_frames_bit_exact(orc):
     np.testing.assert_array_equal(L.tensor("actions", np.int32, (1, 16)), ref["actions"])
 
 
-@pytest.mark.parametrize("T,B", [(2, 16), (3, 32)])
+@pytest.mark.parametrize("T,B", [(2, 16), (3, 32), (2, 7)])  # (2, 7): 21 frames, odd and ragged
 def test_atari_forward_backward_parity(orc, T, B, monkeypatch):
     A = 18
     monkeypatch.setenv("FI_KEEP_DA1", "1")  # the fused conv2/conv1 backward keeps da1 in LDS otherwise
@@ -247,3 +247,38 @@ def test_fc_wgrad_split_matches_single_gemm(monkeypatch):
     rel(a[fcw], b[fcw], "fcW", l2=1e-5, mx=1e-4)
     np.testing.assert_array_equal(a[:fcw.start], b[:fcw.start])
     np.testing.assert_array_equal(a[fcw.stop:], b[fcw.stop:])
+
+
+def test_atari_full_size_sampled_forward_and_determinism(orc):
+    """Bench size (T=100, B=4096: 413,696 frames, every persistent workgroup walking ~1,600
+    frames). Frames are independent in the forward, so 24 frames sampled across the batch must
+    match the oracle's bf16-emulating forward; two learners stepping the same batch must end
+    with bit-identical parameters (fixed-order reductions, process-wide GEMM choices); the
+    step's loss equals the oracle V-trace loss on the GPU's own logits."""
+    T, B, A = 100, 4096, 18
+    N = (T + 1) * B
+    Ls = [mk(T=T, B=B, seed=21, optimizer="adam", lr=5e-4, max_grad_norm=40.0) for _ in range(2)]
+    for L in Ls:
+        L.synth(seed=42)
+    p0 = Ls[0].get_params()
+    st = [L.step_resident() for L in Ls]
+    np.testing.assert_array_equal(Ls[0].get_params(), Ls[1].get_params())
+    assert st[0]["total_loss"] == st[1]["total_loss"]
+    L = Ls[0]
+    idx = np.random.RandomState(3).choice(N, 24, replace=False)
+    idx[:2] = [0, N - 1]
+    frames = L.tensor("frames", np.uint8, (N, 84, 84, 4))[idx]
+    ref = orc.atari_forward(frames, p0, A=A, bf16_emul=True)["out"]
+    logits = L.tensor("logits", shape=(N, A))[idx]
+    values = L.tensor("values", shape=(N,))[idx]
+    rel(logits, ref[:, :A], "logits")
+    rel(values, ref[:, A], "values")
+    lg = L.tensor("logits", shape=(T + 1, B, A))
+    vt = orc.vtrace_loss(lg[:T], L.tensor("mu", shape=(T, B, A)), L.tensor("actions", np.int32, (T, B)),
+                         L.tensor("rewards", shape=(T, B)), L.tensor("discounts", shape=(T, B)),
+                         L.tensor("values", shape=(T + 1, B)))
+    tot = orc.total_loss(vt["losses"])
+    assert abs(st[0]["total_loss"] - tot) <= 1e-5 * max(1.0, abs(tot))
+    assert np.isfinite(L.tensor("grads")).all()
+    for L in Ls:
+        L.close()
