@@ -1778,8 +1778,12 @@ __device__ __forceinline__ void c3_issue(const C3Ctx& c, const uint32_t* tab, in
     }
 }
 
+#ifdef FI_C3_GATHER  // A/B: the gathered-DMA pipeline (3-slot ring, chunk-planar images DMA'd directly)
+namespace c3 {
+constexpr int LDS = RING * SLOT + (XB + DYB) / 16 * 4;
+}  // namespace c3
 // one barrier per frame (see c2_frames); the issuing waves mask their own dY pieces first
-template <class Work>
+template <bool ISSUER, class Work>
 __device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, int nst, Work&& work) {
     const int lane = threadIdx.x & 63, w = wave_id(), tid = threadIdx.x;
     const uint32_t lds0 = lds_addr(smem);
@@ -1826,7 +1830,9 @@ __device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, int nst, W
             m2 = issued;
         }
         PH(2);
+#ifndef FI_EXP_NOWORK3  // timing experiment: data movement only (wrong results)
         work(X, f);
+#endif
         issued += nst;
         PH(3);
         PH_ITER();
@@ -1836,6 +1842,152 @@ __device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, int nst, W
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     PH_FLUSH();
 }
+
+#else
+// Linear-DMA pipeline: every frame's a2, da3 and a3 arrive by LDS-DMA in their own byte order
+// (1 KiB contiguous per wave instruction) into one of two staging buffers; the issuing wave
+// then moves its own landed pieces into the frame's image slot (chunk-planar X, bordered dY),
+// applying the a3 ReLU mask to da3 on the way, so the mask image needs no slot. The gathered
+// DMA straight into the image layouts (FI_C3_GATHER) issued 16-byte pieces at a 128-byte
+// stride: the same bytes, 8x the memory requests (-DFI_EXP_LINDMA, linear sources with wrong
+// layouts: 4.29 -> 3.85 ms).
+// LDS: 2 image slots (X + dY, 28,672 B each; gap / border units zeroed once, never written),
+// 2 staging buffers (a2 11 + da3 7 + a3 7 pieces of 1 KiB), destination tables: 110,624 B.
+namespace c3 {
+constexpr int SLOT2 = XB + DYB;                    // 28,672
+constexpr int NPX = 11, NPD = 7;                   // 1-KiB pieces of a2, of da3 (= of a3)
+constexpr int STGB = (NPX + 2 * NPD) * 1024;       // 25,600
+constexpr int NUX = 10368 / 16, NUD = 6272 / 16;   // 16-B units of a2, of da3
+constexpr int O_STG = 2 * SLOT2, O_TAB = O_STG + 2 * STGB;
+constexpr int LDS = O_TAB + (NUX + NUD) * 2;       // 110,624
+}  // namespace c3
+
+// ISSUER: waves 0-3 (compile-time role, so the data-gradient waves carry none of the DMA /
+// reshuffle code); wave w owns a2 pieces w + 4i (< 11) and da3 / a3 pieces w + 4i (< 7)
+template <bool ISSUER, class Work>
+__device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, int nst, Work&& work) {
+    const int lane = threadIdx.x & 63, w = wave_id(), tid = threadIdx.x;
+    const uint32_t lds0 = lds_addr(smem);
+    uint16_t* dstx = (uint16_t*)(smem + c3::O_TAB);
+    uint16_t* dsty = dstx + c3::NUX;
+    for (int i = tid; i < 2 * c3::SLOT2 / 16; i += 512) ((u32x4*)smem)[i] = u32x4{0, 0, 0, 0};
+    for (int i = tid; i < c3::NUX; i += 512) {  // a2 unit (pixel p, chunk cc) -> X image unit
+        const int p = i >> 3, cc = i & 7;
+        dstx[i] = (uint16_t)(p + 96 * cc + c3::zc(cc));
+    }
+    for (int i = tid; i < c3::NUD; i += 512) {  // da3 unit (pixel (y, x), chunk cc) -> bordered dY unit
+        const int q = i >> 3, cc = i & 7, y = q / 7, x = q - 7 * y;
+        dsty[i] = (uint16_t)(9 * (y + 2) + (x + 2) + 128 * cc + c3::zc(cc));
+    }
+    __syncthreads();
+    const int nmine = c.nframes > (int)blockIdx.x ? (c.nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+    auto issue = [&](int k, int sb) {  // frame k's pieces of this wave into staging sb
+        const int f = blockIdx.x + k * gridDim.x;
+        const fi_i32x4 xr = make_rsrc(c.a2 + (size_t)f * 5184, 10368);
+        const fi_i32x4 dr = make_rsrc(c.da3 + (size_t)f * 3136, 6272);
+        const fi_i32x4 mr = make_rsrc(c.a3 + (size_t)f * 3136, 6272);
+        const uint32_t base = lds0 + c3::O_STG + sb * c3::STGB;
+        int n = 0;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const int j = w + 4 * i;
+            if (j < c3::NPX) {
+                blds16(xr, 1024 * j + 16 * lane, base + 1024 * j);
+                ++n;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int j = w + 4 * i;
+            if (j < c3::NPD) {
+                blds16(dr, 1024 * j + 16 * lane, base + 1024 * (c3::NPX + j));
+                blds16(mr, 1024 * j + 16 * lane, base + 1024 * (c3::NPX + c3::NPD + j));
+                n += 2;
+            }
+        }
+        return n;
+    };
+    auto reshuffle = [&](int sb, int slot) {  // own landed pieces -> image slot (a2, then da3: reads, then writes)
+        const char* st = smem + c3::O_STG + sb * c3::STGB;
+        char* im = smem + slot * c3::SLOT2;
+        {
+            u32x4 xv[3];
+            int xd[3];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                const int u = min(64 * (w + 4 * i) + lane, c3::NUX - 1);
+                xv[i] = *(const u32x4*)(st + 16 * u);
+                xd[i] = dstx[u];
+            }
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+                if (64 * (w + 4 * i) + lane < c3::NUX) *(u32x4*)(im + 16 * xd[i]) = xv[i];
+        }
+        s16x8 dv[2], mv[2];
+        int dd[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int u = min(64 * (w + 4 * i) + lane, c3::NUD - 1);
+            dv[i] = *(const s16x8*)(st + 1024 * c3::NPX + 16 * u);
+            mv[i] = *(const s16x8*)(st + 1024 * (c3::NPX + c3::NPD) + 16 * u);
+            dd[i] = dsty[u];
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            if (64 * (w + 4 * i) + lane < c3::NUD) {
+                s16x8 v = dv[i];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) v[q] = mv[i][q] > 0 ? v[q] : (short)0;
+                *(s16x8*)(im + c3::XB + 16 * dd[i]) = v;
+            }
+    };
+    // frame k: staging k % 2, image slot k & 1. mA / mB: this wave's issue count right after the
+    // DMA of the next / next-but-one frame to reshuffle.
+    int issued = 0, mA = 0, mB = 0;
+    if constexpr (ISSUER) {
+        int m0 = 0;
+        if (nmine > 0) issued += issue(0, 0);
+        m0 = issued;
+        if (nmine > 1) issued += issue(1, 1);
+        mA = issued;
+        if (nmine > 0) {
+            wait_vmcnt(issued - m0);
+            reshuffle(0, 0);
+        }
+        if (nmine > 2) issued += issue(2, 0);
+        mB = issued;
+    }
+    PH_DECL
+    for (int it = 0; it < nmine; ++it) {
+        const int f = blockIdx.x + it * gridDim.x;
+        char* X = smem + (it & 1) * c3::SLOT2;
+        PH(5);
+        lds_barrier();  // frame it in slot it&1; every wave done with frame it-1 (slot (it+1)&1)
+        PH(1);
+        if (ISSUER && it + 1 < nmine) {
+            wait_vmcnt(issued - mA);  // own pieces of frame it+1 landed
+            PH(0);
+            reshuffle((it + 1) & 1, (it + 1) & 1);
+            int mC = issued;
+            if (it + 3 < nmine) {
+                issued += issue(it + 3, (it + 1) & 1);  // into the staging buffer just emptied
+                mC = issued;
+            }
+            mA = mB;
+            mB = mC;
+        }
+        PH(2);
+#ifndef FI_EXP_NOWORK3  // timing experiment: data movement only (wrong results)
+        work(X, f);
+#endif
+        issued += nst;
+        PH(3);
+        PH_ITER();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    PH_FLUSH();
+}
+#endif
 
 // weight gradient of one wave, taps t = 2i + B (B = wr>>1), i < 5 - B
 template <int B>
@@ -1850,7 +2002,7 @@ __device__ __forceinline__ void c3_wgrad(const C3Ctx& ctx, char* smem, float* sl
 #pragma unroll
     for (int i = 0; i < NKT; ++i) { accw[i][0] = f32x16{}; accw[i][1] = f32x16{}; }
     float bsum0 = 0.f, bsum1 = 0.f;
-    c3_frames(ctx, smem, 0, [&](const char* X, int) {
+    c3_frames<true>(ctx, smem, 0, [&](const char* X, int) {
         const char* XA = X + ba0;
         const char* XB_ = X + bb0;
         bf16x8 fb[2][NKT + 2];  // [0] b0, [1] b1 (co halves), [2 + i] A of tap 2i + B
@@ -1921,7 +2073,7 @@ __global__ __launch_bounds__(512, 2) void conv3_bwd_fr(const __bf16* __restrict_
                                                        float* __restrict__ slab,     // [grid][576][64]
                                                        float* __restrict__ cs_slab,  // [grid][64]
                                                        int nframes) {
-    __shared__ __attribute__((aligned(16))) char smem[c3::RING * c3::SLOT + (c3::XB + c3::DYB) / 16 * 4];
+    __shared__ __attribute__((aligned(16))) char smem[c3::LDS];
     const int lane = threadIdx.x & 63;
     const int w = wave_id(), wr = w & 3;
     const int g = lane >> 4;
@@ -2014,9 +2166,9 @@ __global__ __launch_bounds__(512, 2) void conv3_bwd_fr(const __bf16* __restrict_
             }
         };
 #ifdef FI_EXP_NODX
-        c3_frames(ctx, smem, 0, [&](const char* X, int f) {
+        c3_frames<false>(ctx, smem, 0, [&](const char* X, int f) {
 #else
-        c3_frames(ctx, smem, 3, [&](const char* X, int f) {
+        c3_frames<false>(ctx, smem, 3, [&](const char* X, int f) {
 #endif
             if (ph) work(std::integral_constant<int, 1>{}, X, f);
             else work(std::integral_constant<int, 0>{}, X, f);
