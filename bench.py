@@ -165,11 +165,15 @@ def main():
     from freeimpala_amd.learner import DeviceLearner
 
     T, B, A = args.seq_len, args.batch, args.num_actions
-    L = DeviceLearner(args.arch, seq_len=T, batch=B, num_actions=A, device=local,
+    # rehearsal knobs for a one-GPU box (never set by the driver): FI_BENCH_DEVICE pins every
+    # rank to one device, FI_BENCH_NO_COMM skips the RCCL communicator (RCCL refuses two ranks
+    # on one device), so the launcher path (torchrun env, gloo, shards, barrier, max) runs
+    device = int(os.environ.get("FI_BENCH_DEVICE", local))
+    L = DeviceLearner(args.arch, seq_len=T, batch=B, num_actions=A, device=device,
                       optimizer="adam", publish="bf16" if args.arch == "atari" else "fp32")
     b_off, _ = shard_columns(rank, N, B)
     L.synth(seed=42, b_global=B * N, b_offset=b_off)
-    if ws > 1:  # RCCL communicator for the in-step gradient all-reduce (uid via gloo)
+    if ws > 1 and not os.environ.get("FI_BENCH_NO_COMM"):  # RCCL communicator for the in-step gradient all-reduce (uid via gloo)
         uid = broadcast_bytes(DeviceLearner.comm_unique_id() if rank == 0 else b"", 0)
         L.attach_comm(uid, rank, ws)
 

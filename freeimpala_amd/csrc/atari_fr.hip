@@ -1340,7 +1340,11 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
     const int g = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3, h = lane >> 5, col = lane & 31;
     const uint32_t lds0 = lds_addr(smem);
     uint32_t* tab = (uint32_t*)(smem + c21::O_TAB);
+#ifdef FI_EXP_LINDMA21  // timing experiment: coalesced linear DMA sources (wrong results)
+    for (int i = tid; i < (c2::XB + c2::DYB) / 16; i += 512) tab[i] = i < c2::XB / 16 ? 16 * i : (16 * (i - c2::XB / 16) < 10368 ? 16 * (i - c2::XB / 16) : FI_OOB);
+#else
     for (int i = tid; i < (c2::XB + c2::DYB) / 16; i += 512) tab[i] = i < c2::XB / 16 ? c2_x_src(i) : c2_dy_src(i - c2::XB / 16);
+#endif
     char* DY = smem + c21::O_DY;
     char* IMG = smem + c21::O_IMG;
     char* D = smem + c21::O_D;
