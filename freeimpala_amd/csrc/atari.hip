@@ -728,6 +728,7 @@ struct AtariImpl {
     bool fuse12 = true;    // conv1+conv2 forward in one kernel (FI_FWD_UNFUSED=1 -> two kernels)
     bool fuse21 = true;    // conv2 backward + conv1 wgrad in one kernel (FI_BWD_UNFUSED=1 -> two)
     bool keep_da1 = false; // fused backward also stores da1 to HBM (FI_KEEP_DA1=1; parity checks)
+    bool a1_planar = true; // fused fwd + bwd: a1 stored in conv21's image order (FI_A1_NHWC=1 -> NHWC)
     FcBlasLt* fc = nullptr;  // fc layer GEMMs (hipBLASLt)
 };
 
@@ -738,12 +739,13 @@ int conv2_fwd_fr_launch(const __bf16* a1, const __bf16* w2t, const float* bias, 
 int conv3_fwd_fr_launch(const __bf16* a2, const __bf16* w3t, const float* bias, __bf16* a3, int nframes,
                         int grid, hipStream_t s);
 int conv12_fwd_fr_launch(const uint8_t* frames, const __bf16* w1t, const float* b1, const __bf16* w2t,
-                         const float* b2, __bf16* a1, __bf16* a2, int nframes, int grid, hipStream_t s);
+                         const float* b2, __bf16* a1, __bf16* a2, int nframes, int grid, hipStream_t s,
+                         int a1_planar);
 int conv1_wgrad_fr_launch(const uint8_t* frames, const __bf16* da1, float* slab, float* cs_slab,
                           int nframes, int grid, hipStream_t s);
 int conv21_bwd_fr_launch(const __bf16* a1, const __bf16* da2, const __bf16* w2d, const uint8_t* frames,
                          __bf16* da1_out, float* slab2, float* cs2, float* slab1, float* cs1, int nframes,
-                         int grid, hipStream_t s);
+                         int grid, hipStream_t s, int a1_planar);
 int conv2_bwd_fr_launch(const __bf16* a1, const __bf16* da2, const __bf16* w2d, __bf16* da1, float* slab,
                         float* cs_slab, int nframes, int grid, hipStream_t s);
 int conv3_bwd_fr_launch(const __bf16* a2, const __bf16* da3, const __bf16* a3, const __bf16* w3d, __bf16* da2,
@@ -781,6 +783,8 @@ AtariNet* atari_create(int B, int T, int A) {
     I->fuse12 = std::getenv("FI_FWD_UNFUSED") == nullptr;
     I->fuse21 = std::getenv("FI_BWD_UNFUSED") == nullptr;
     I->keep_da1 = std::getenv("FI_KEEP_DA1") != nullptr;
+    // only conv21_bwd_fr reads a1 when both fused kernels run; every other consumer wants NHWC
+    I->a1_planar = I->fr && I->fuse12 && I->fuse21 && std::getenv("FI_A1_NHWC") == nullptr;
     I->cs2 = (int)(((N * 100) + GBM - 1) / GBM * GBM);
     I->cs3 = (int)(((N * 81) + GBM - 1) / GBM * GBM);
     bool ok = dmalloc(I, &I->a1, N * 400 * 32) && dmalloc(I, &I->a2, N * 81 * 64) &&
@@ -848,7 +852,7 @@ int atari_forward(AtariNet* n, const uint8_t* frames, float* logits, float* valu
     if (I->fr && I->fuse12) {
         TagScope ts(tg, "conv12_fwd");
         rc = conv12_fwd_fr_launch(frames, I->wb.c1T, p + o.c1b, I->wb.c2T, p + o.c2b, I->a1, I->a2, N,
-                                  std::min(N, FR_GRID), s);
+                                  std::min(N, FR_GRID), s, I->a1_planar);
     } else if (I->fr) {
         TagScope ts(tg, "conv1_fwd");
         rc = conv1_fwd_fr_launch(frames, I->wb.c1T, p + o.c1b, I->a1, N, std::min(N, FR_GRID), s);
@@ -931,7 +935,7 @@ int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, con
         float* slab1 = slab + (size_t)grid * C2K * C2O;
         float* cs1 = cs + (size_t)grid * C2O;
         FI_A("conv21_bwd", conv21_bwd_fr_launch(I->a1, I->da2, I->wb.c2D, frames, I->keep_da1 ? I->da1 : nullptr,
-                                                slab, cs, slab1, cs1, N, grid, s));
+                                                slab, cs, slab1, cs1, N, grid, s, I->a1_planar));
         FI_A("reduce_slabs", reduce_slabs(slab, grid, (size_t)C2K * C2O, grads + o.c2w, s));
         FI_A("reduce_slabs", reduce_slabs(cs, grid, (size_t)C2O, grads + o.c2b, s));
         FI_A("reduce_slabs", reduce_slabs(slab1, grid, (size_t)C1K * C1O, grads + o.c1w, s));

@@ -769,7 +769,7 @@ __global__ __launch_bounds__(512, 2) void conv12_fwd_fr(const uint8_t* __restric
                                                         const __bf16* __restrict__ w2t,  // [64][512]
                                                         const float* __restrict__ b2,
                                                         __bf16* __restrict__ a1, __bf16* __restrict__ a2,
-                                                        int nframes) {
+                                                        int nframes, int a1_planar) {
     __shared__ __attribute__((aligned(16))) char smem[c12::LDS];
     char* img = smem + 2 * c1::RAW;
     char* x2 = img + c1::IMG;
@@ -842,7 +842,13 @@ __global__ __launch_bounds__(512, 2) void conv12_fwd_fr(const uint8_t* __restric
                             o[4 + r] = (__bf16)fmaxf(db[r] * inv255 + bch[4 + r], 0.f);
                         }
                         held[tt] = __builtin_bit_cast(u32x4, o);
-                        FI_ST16(held[tt], dst + 4 * (t * 16 + si) + g);
+                        // a1 in HBM: NHWC, or (a1_planar) in conv21's image order -- parity-class
+                        // plane P = 2(iy&1) + (ix&1), position (iy>>1)*10 + (ix>>1), chunk g -- so
+                        // that conv21 loads it by linear DMA (c2_x_src)
+                        const int q = t * 16 + si, iy = q / 20, ix = q - 20 * iy;
+                        const int u = a1_planar ? 400 * (2 * (iy & 1) + (ix & 1)) + 4 * ((iy >> 1) * 10 + (ix >> 1)) + g
+                                                : 4 * q + g;
+                        FI_ST16(held[tt], dst + u);
                     }
                 }
             }
@@ -952,8 +958,10 @@ __global__ __launch_bounds__(512, 2) void conv12_fwd_fr(const uint8_t* __restric
 }
 
 int conv12_fwd_fr_launch(const uint8_t* frames, const __bf16* w1t, const float* b1, const __bf16* w2t,
-                         const float* b2, __bf16* a1, __bf16* a2, int nframes, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(conv12_fwd_fr, dim3(grid), dim3(512), 0, s, frames, w1t, b1, w2t, b2, a1, a2, nframes);
+                         const float* b2, __bf16* a1, __bf16* a2, int nframes, int grid, hipStream_t s,
+                         int a1_planar) {
+    hipLaunchKernelGGL(conv12_fwd_fr, dim3(grid), dim3(512), 0, s, frames, w1t, b1, w2t, b2, a1, a2, nframes,
+                       a1_planar);
     FI_HIP_CHECK(hipGetLastError());
     ph_report("conv12_fwd", grid);
     return FI_OK;
@@ -999,7 +1007,7 @@ namespace c2 {
 constexpr int XB = 20 * 20 * 64;             // 25,600: a1 image (class planes)
 constexpr int DYB = 16 * 1024;               // 1,019 used units of 16 B -> 16 KiB
 constexpr int SLOT = XB + DYB;               // 41,984
-constexpr int RING = 3;
+[[maybe_unused]] constexpr int RING = 3;
 constexpr int NX = XB / 1024, NDY = DYB / 1024;  // 25 + 16 pieces
 static_assert(NX + NDY == 41, "c2_issue assigns 10 pieces to each of waves 0-3 + 1 to wave 0");
 __host__ __device__ constexpr int zc(int c) { return 8 * (c & 1) + 4 * ((c >> 1) & 1); }
@@ -1333,7 +1341,7 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                                                         float* __restrict__ cs2,       // [grid][64]
                                                         float* __restrict__ slab1,     // [grid][256][32]
                                                         float* __restrict__ cs1,       // [grid][4 classes][32]
-                                                        int nframes) {
+                                                        int nframes, int a1_planar) {
     __shared__ __attribute__((aligned(16))) char smem[c21::LDS];
     const int lane = threadIdx.x & 63, tid = threadIdx.x;
     const int w = wave_id(), wr = w & 3;
@@ -1343,7 +1351,10 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
 #ifdef FI_EXP_LINDMA21  // timing experiment: coalesced linear DMA sources (wrong results)
     for (int i = tid; i < (c2::XB + c2::DYB) / 16; i += 512) tab[i] = i < c2::XB / 16 ? 16 * i : (16 * (i - c2::XB / 16) < 10368 ? 16 * (i - c2::XB / 16) : FI_OOB);
 #else
-    for (int i = tid; i < (c2::XB + c2::DYB) / 16; i += 512) tab[i] = i < c2::XB / 16 ? c2_x_src(i) : c2_dy_src(i - c2::XB / 16);
+    // a1 planar (conv12_fwd_fr wrote it in this image's order): the a1 pieces are linear 1-KiB
+    // runs; NHWC: 16-byte gathers at a 128-byte stride
+    for (int i = tid; i < (c2::XB + c2::DYB) / 16; i += 512)
+        tab[i] = i < c2::XB / 16 ? (a1_planar ? 16u * i : c2_x_src(i)) : c2_dy_src(i - c2::XB / 16);
 #endif
     char* DY = smem + c21::O_DY;
     char* IMG = smem + c21::O_IMG;
@@ -1704,13 +1715,13 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
 
 int conv21_bwd_fr_launch(const __bf16* a1, const __bf16* da2, const __bf16* w2d, const uint8_t* frames,
                          __bf16* da1_out, float* slab2, float* cs2, float* slab1, float* cs1, int nframes,
-                         int grid, hipStream_t s) {
+                         int grid, hipStream_t s, int a1_planar) {
     if (da1_out)
         hipLaunchKernelGGL(conv21_bwd_fr<true>, dim3(grid), dim3(512), 0, s, a1, da2, w2d, frames, da1_out, slab2,
-                           cs2, slab1, cs1, nframes);
+                           cs2, slab1, cs1, nframes, a1_planar);
     else
-        hipLaunchKernelGGL(conv21_bwd_fr<false>, dim3(grid), dim3(512), 0, s, a1, da2, w2d, frames, da1_out, slab2, cs2,
-                       slab1, cs1, nframes);
+        hipLaunchKernelGGL(conv21_bwd_fr<false>, dim3(grid), dim3(512), 0, s, a1, da2, w2d, frames, da1_out, slab2,
+                           cs2, slab1, cs1, nframes, a1_planar);
     FI_HIP_CHECK(hipGetLastError());
     ph_report("conv21_bwd", grid);
     return FI_OK;
@@ -1737,8 +1748,8 @@ namespace c3 {
 constexpr int XB = 12 * 1024;                // 768 units (8 chunk planes of 96)
 constexpr int DYB = 16 * 1024;               // 1,009 used units -> 16 KiB
 constexpr int MB = 16 * 1024;                // a3 image, same layout as dY
-constexpr int SLOT = XB + DYB + MB;          // 45,056
-constexpr int RING = 3;
+[[maybe_unused]] constexpr int SLOT = XB + DYB + MB;  // 45,056 (FI_C3_GATHER)
+[[maybe_unused]] constexpr int RING = 3;
 constexpr int NX = XB / 1024, NDY = DYB / 1024;  // 12 + 16 (+ 16 mask) pieces
 static_assert(NX == 12 && NDY == 16, "c3_issue assigns 3 X + 4 dY + 4 mask pieces per wave");
 __host__ __device__ constexpr int zc(int c) { return 8 * (c & 1) + 4 * ((c >> 1) & 1); }

@@ -45,6 +45,7 @@ def test_atari_synth_frames_bit_exact(orc):
 def test_atari_forward_backward_parity(orc, T, B, monkeypatch):
     A = 18
     monkeypatch.setenv("FI_KEEP_DA1", "1")  # the fused conv2/conv1 backward keeps da1 in LDS otherwise
+    monkeypatch.setenv("FI_A1_NHWC", "1")   # a1 in NHWC (the fused pair stores it in conv21's image order)
     L = mk(T=T, B=B, A=A)
     L.synth(seed=T * 100 + B)
     N = (T + 1) * B
@@ -132,6 +133,7 @@ def test_frame_resident_kernels_match_generic_path(monkeypatch):
     T, B = 2, 16
     outs = {}
     monkeypatch.setenv("FI_KEEP_DA1", "1")
+    monkeypatch.setenv("FI_A1_NHWC", "1")
     for mode in ("generic", "fr"):
         if mode == "generic":
             monkeypatch.setenv("FI_ATARI_GENERIC", "1")
@@ -165,6 +167,7 @@ def test_fused_conv12_forward_matches_separate_kernels(monkeypatch):
     persistent workgroup, so the pipeline's steady state (raw ring, role hand-off) is covered."""
     T, B = 5, 176
     outs = {}
+    monkeypatch.setenv("FI_A1_NHWC", "1")
     for mode in ("unfused", "fused"):
         if mode == "unfused":
             monkeypatch.setenv("FI_FWD_UNFUSED", "1")
@@ -282,3 +285,34 @@ def test_atari_full_size_sampled_forward_and_determinism(orc):
     assert np.isfinite(L.tensor("grads")).all()
     for L in Ls:
         L.close()
+
+
+def a1_planar_to_nhwc(a):
+    """conv21's image order (parity-class plane P = 2(iy&1) + (ix&1), position (iy>>1)*10 +
+    (ix>>1), 32 channels) -> NHWC (N, 20, 20, 32)."""
+    N = a.shape[0]
+    p = a.reshape(N, 2, 2, 10, 10, 32)  # [P>>1][P&1][iy>>1][ix>>1]
+    return p.transpose(0, 3, 1, 4, 2, 5).reshape(N, 20, 20, 32)
+
+
+def test_a1_planar_layout_matches_nhwc(monkeypatch):
+    """The fused forward + backward pair stores a1 in conv21's image order (linear DMA there);
+    against the NHWC store (FI_A1_NHWC) a1 is the same tensor permuted, and every gradient and
+    the updated parameters are bit-identical. 4-5 frames per workgroup."""
+    T, B = 5, 176
+    N = (T + 1) * B
+    outs = {}
+    for mode in ("nhwc", "planar"):
+        if mode == "nhwc":
+            monkeypatch.setenv("FI_A1_NHWC", "1")
+        else:
+            monkeypatch.delenv("FI_A1_NHWC", raising=False)
+        L = mk(T=T, B=B, seed=8)
+        L.synth(seed=31)
+        L.step_resident()
+        outs[mode] = dict(a1=L.tensor("a1", np.uint16, (N, 12800)), g=L.tensor("grads"), p=L.get_params())
+        L.close()
+    np.testing.assert_array_equal(a1_planar_to_nhwc(outs["planar"]["a1"]),
+                                  outs["nhwc"]["a1"].reshape(N, 20, 20, 32))
+    np.testing.assert_array_equal(outs["planar"]["g"], outs["nhwc"]["g"])
+    np.testing.assert_array_equal(outs["planar"]["p"], outs["nhwc"]["p"])
