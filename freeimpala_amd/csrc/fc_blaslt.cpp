@@ -170,6 +170,11 @@ static int make_gemm(FcBlasLt* F, FcGemm& G, int m, int n, int k, bool ta, bool 
             }
         }
     }
+    if (std::getenv("FI_DETERMINISTIC")) {  // no timing: the heuristic's first solution, so every
+        G.algo = cands[0].algo;             // process picks the same kernels (run-to-run bit-exact)
+        if (best_ms) *best_ms = 0.f;
+        return FI_OK;
+    }
     auto tuned = kSweepBest.find({m, n, k, ta, tb, batch});
     if (tuned != kSweepBest.end() && !std::getenv("FI_BLT_NO_SWEEP")) add_by_index(tuned->second);
     // time the candidates once (the tensors hold hashed data at creation; only speed matters)
@@ -286,8 +291,8 @@ FcBlasLt* fc_blaslt_create(int rows, const void* a3, const void* w, const void* 
     // form 0 direct, 1 transposed, 2 + i split i: the process-wide choice for this row count
     // (every handle of the process then computes bit-identical gradients), else a tournament:
     // 2 rounds x 4 timed runs of each complete form (GEMM + transpose / partial sum), min kept
-    int form = -1;
-    if (rc == FI_OK) {
+    int form = std::getenv("FI_DETERMINISTIC") ? 0 : -1;  // deterministic mode: dW directly
+    if (rc == FI_OK && form < 0) {
         std::lock_guard<std::mutex> lk(g_algo_mu);
         auto it = g_wgrad_form.find(rows);
         if (it != g_wgrad_form.end()) {

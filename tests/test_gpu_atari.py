@@ -316,3 +316,22 @@ def test_a1_planar_layout_matches_nhwc(monkeypatch):
                                   outs["nhwc"]["a1"].reshape(N, 20, 20, 32))
     np.testing.assert_array_equal(outs["planar"]["g"], outs["nhwc"]["g"])
     np.testing.assert_array_equal(outs["planar"]["p"], outs["nhwc"]["p"])
+
+
+def test_deterministic_mode_is_bit_exact_across_processes(tmp_path):
+    """The fc GEMM algorithms are chosen by timing at creation (per process), so two runs can
+    round differently; FI_DETERMINISTIC=1 takes the heuristic's first solution and the direct
+    weight-gradient form instead: two separate processes then produce the same gradient blob
+    bit for bit."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, FI_DETERMINISTIC="1")
+    outs = []
+    for i in range(2):
+        f = tmp_path / f"g{i}.npy"
+        subprocess.run([sys.executable, os.path.join(root, "scripts", "grads_dump.py"), str(f)], env=env,
+                       check=True, timeout=240)
+        outs.append(np.load(f))
+    np.testing.assert_array_equal(outs[0], outs[1])
