@@ -45,7 +45,7 @@ int f32_heads_wgrad_partial(const float* X, int I, const HeadsGrad& g, int split
 // misc.hip
 int colsum_partial(const float* Y, int M, int N, int splits, float* slab, hipStream_t s);
 int heads_colsum_partial(const HeadsGrad& g, int splits, float* slab, hipStream_t s);
-int reduce_slabs(const float* slab, int splits, size_t count, float* out, hipStream_t s);
+int reduce_slabs(float* slab, int splits, size_t count, float* out, hipStream_t s);  // slab is scratch (overwritten)
 // squared L2 norm of g -> *out; optionally also sums vt_nblk V-trace loss partials [i][3]
 // into vt_losses[0..2] in the same (final) launch
 int grad_sqnorm(const float* g, size_t n, double* part, int nblk, double* out, hipStream_t s,

@@ -208,8 +208,9 @@ int heads_colsum_partial(const HeadsGrad& g, int splits, float* slab, hipStream_
 // out[i] = sum_k slab[k][i] over `splits` fp32 partial slabs, in a fixed order (deterministic):
 // a block owns 64 consecutive outputs (one per lane); its 4 waves take the splits k = w mod 4
 // (4 independent accumulators each) and their partials are combined in wave order.
+// out[i] = sum over k < splits of slab[k * stride + i], in a fixed order (deterministic)
 __global__ __launch_bounds__(256) void reduce_slabs_kernel(const float* __restrict__ slab, int splits,
-                                                           size_t count, float* __restrict__ out) {
+                                                           size_t count, size_t stride, float* __restrict__ out) {
     __shared__ float red[4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const size_t i = (size_t)blockIdx.x * 64 + lane;
@@ -217,21 +218,49 @@ __global__ __launch_bounds__(256) void reduce_slabs_kernel(const float* __restri
     if (i < count) {
         int k = w;
         for (; k + 12 < splits; k += 16) {
-            a0 += slab[(size_t)k * count + i];
-            a1 += slab[(size_t)(k + 4) * count + i];
-            a2 += slab[(size_t)(k + 8) * count + i];
-            a3 += slab[(size_t)(k + 12) * count + i];
+            a0 += slab[(size_t)k * stride + i];
+            a1 += slab[(size_t)(k + 4) * stride + i];
+            a2 += slab[(size_t)(k + 8) * stride + i];
+            a3 += slab[(size_t)(k + 12) * stride + i];
         }
-        for (; k < splits; k += 4) a0 += slab[(size_t)k * count + i];
+        for (; k < splits; k += 4) a0 += slab[(size_t)k * stride + i];
     }
     red[w][lane] = (a0 + a1) + (a2 + a3);
     __syncthreads();
     if (w == 0 && i < count) out[i] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
 
-int reduce_slabs(const float* slab, int splits, size_t count, float* out, hipStream_t s) {
-    hipLaunchKernelGGL(reduce_slabs_kernel, dim3((unsigned)((count + 63) / 64)), dim3(256), 0, s, slab, splits,
-                       count, out);
+// first stage for narrow slabs (few outputs, many partials): block (x, g) sums rows
+// [32g, 32g + 32) of 64 outputs in a fixed order and leaves the partial in row 32g (the slab
+// is scratch: every element is read and rewritten by one thread only)
+constexpr int kSlabGroup = 32;
+__global__ __launch_bounds__(64) void reduce_slabs_stage1(float* __restrict__ slab, int splits, size_t count) {
+    const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
+    if (i >= count) return;
+    const int k0 = blockIdx.y * kSlabGroup, k1 = min(splits, k0 + kSlabGroup);
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int k = k0;
+    for (; k + 3 < k1; k += 4) {
+        a0 += slab[(size_t)k * count + i];
+        a1 += slab[(size_t)(k + 1) * count + i];
+        a2 += slab[(size_t)(k + 2) * count + i];
+        a3 += slab[(size_t)(k + 3) * count + i];
+    }
+    for (; k < k1; ++k) a0 += slab[(size_t)k * count + i];
+    slab[(size_t)k0 * count + i] = (a0 + a1) + (a2 + a3);
+}
+
+int reduce_slabs(float* slab, int splits, size_t count, float* out, hipStream_t s) {
+    if (splits >= 4 * kSlabGroup && count < 32768) {  // narrow: one block per 64 outputs would
+        const int groups = (splits + kSlabGroup - 1) / kSlabGroup;  // walk all splits serially
+        hipLaunchKernelGGL(reduce_slabs_stage1, dim3((unsigned)((count + 63) / 64), (unsigned)groups), dim3(64), 0, s,
+                           slab, splits, count);
+        hipLaunchKernelGGL(reduce_slabs_kernel, dim3((unsigned)((count + 63) / 64)), dim3(256), 0, s, slab, groups,
+                           count, (size_t)kSlabGroup * count, out);
+    } else {
+        hipLaunchKernelGGL(reduce_slabs_kernel, dim3((unsigned)((count + 63) / 64)), dim3(256), 0, s, slab, splits,
+                           count, count, out);
+    }
     FI_HIP_CHECK(hipGetLastError());
     return FI_OK;
 }
