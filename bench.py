@@ -214,6 +214,13 @@ def main():
     if os.path.exists(tpath) and (T, B, A) == (100, 4096, 18):
         with open(tpath) as fh:
             traffic = {k: v["hbm_bytes_per_launch"] for k, v in json.load(fh).items() if not k.startswith("_")}
+    # MFMA utilisation and effective clock per kernel from the committed counter pass
+    # (scripts/pmc_mfma.sh), same config only
+    mfma = {}
+    mpath = os.path.join(ROOT, "profiles", f"r01_pmc_mfma_{args.arch}.json")
+    if os.path.exists(mpath) and (T, B, A) == (100, 4096, 18):
+        with open(mpath) as fh:
+            mfma = {k: v for k, v in json.load(fh).items() if not k.startswith("_")}
     per_step = {k: v["ms"] * v["count"] / max(1, args.profile_steps) for k, v in kt.items()}
     dominant = max(per_step, key=per_step.get) if per_step else None
     dtype = "bf16" if args.arch == "atari" else "fp32"
@@ -227,6 +234,8 @@ def main():
         peak_f = MFMA_PEAK_TFLOPS[dtype] * 1e12
         t_mfma, t_hbm = flops / peak_f, nbytes / (HBM_PEAK_GBS * 1e9)
         common = {"kernel": name, "traffic": tr, "launch_ms": round(ms, 5),
+                  "mfma_util_pmc": mfma.get(name, {}).get("mfma_util"),
+                  "clock_mhz_pmc": mfma.get(name, {}).get("clock_mhz"),
                   "algorithmic_flops": flops, "algorithmic_bytes": nbytes,
                   "time_at_peak_ms": {"mfma": round(t_mfma * 1e3, 4), "hbm": round(t_hbm * 1e3, 4)}}
         if t_hbm >= t_mfma:
