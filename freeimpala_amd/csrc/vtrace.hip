@@ -181,14 +181,23 @@ struct VtLayout {
     static constexpr int LOGB = TC * ROWB;             // bytes per logits tile (= 256*NW*A)
     static constexpr int SCB = TC * NB * 4;            // bytes per scalar tile (= 256*NW)
     static constexpr int PT = LOGB / 1024;             // 1-KiB pieces per logits tile
-    static constexpr int SLOT = 2 * LOGB + 4 * SCB;    // pi | mu | act | rew | disc | val
+#ifdef FI_VT_MUREG  // mu rows go straight to registers (one chunk ahead): half the LDS per wave
+    static constexpr int MUB = 0;                      // no mu tile
+    static constexpr int TOTB = NW * 16 * 4;           // per-slot wave totals (d, g per column)
+    static constexpr int GLOG = (PT + NW - 1) / NW;    // pi pieces per wave per chunk (j < PT)
+#else
+    static constexpr int MUB = LOGB;
+    static constexpr int TOTB = 0;
+    static constexpr int GLOG = 2 * PT / NW;           // logits pieces per wave per chunk
+#endif
+    static constexpr int SCO = LOGB + MUB;             // scalar tiles' offset in a slot
+    static constexpr int SLOT = SCO + 4 * SCB + TOTB;  // pi | mu | act | rew | disc | val [| tot]
     static constexpr int RING = 2;
     static constexpr int TOTAL = RING * SLOT;
-    static constexpr int GLOG = 2 * PT / NW;           // logits pieces per wave per chunk
     static constexpr int WPS0 = (163840 / TOTAL) * NW / 4;  // waves per SIMD the LDS allows
     static constexpr int WPS = WPS0 < 1 ? 1 : (WPS0 > 8 ? 8 : WPS0);
     static_assert(A % 2 == 0, "fast V-trace kernel needs even A");
-    static_assert((NW == 2 || NW == 4) && LOGB % 1024 == 0 && (2 * PT) % NW == 0, "tiling");
+    static_assert((NW == 2 || NW == 4) && LOGB % 1024 == 0 && (2 * PT) % NW == 0 && SCB == 256 * NW, "tiling");
     static_assert(TOTAL <= 160 * 1024, "LDS budget");
 };
 
@@ -214,6 +223,9 @@ __device__ __forceinline__ int vt_issue_chunk(const VtArgs& a, const VtRsrc& rs,
 #pragma unroll
     for (int i = I0; i < (I1 < L::GLOG ? I1 : L::GLOG); ++i) {
         const int j = w + L::NW * i;  // wave-uniform piece index: pi (0..PT-1), mu (PT..2PT-1)
+#ifdef FI_VT_MUREG
+        if (j >= L::PT) continue;     // pi pieces only
+#endif
         const int jj = j < L::PT ? j : j - L::PT;
         const int last_row = (jj * 1024 + 1023) / L::ROWB;
         if (last_row < first_row) continue;
@@ -234,13 +246,13 @@ __device__ __forceinline__ int vt_issue_chunk(const VtArgs& a, const VtRsrc& rs,
         // the piece's 4/NW tiles come from up to 4 tensors: one descriptor per tile, lanes select
         const uint32_t off = (uint32_t)((t * a.B + b0) * 4 + (lane & 1) * 16);
         if constexpr (L::NW == 4) {
-            blds16(w == 0 ? rs.act : w == 1 ? rs.rew : w == 2 ? rs.disc : rs.val, off, base + 2 * L::LOGB + w * 1024);
+            blds16(w == 0 ? rs.act : w == 1 ? rs.rew : w == 2 ? rs.disc : rs.val, off, base + L::SCO + w * 1024);
         } else {
             const char* arr = s == 0 ? (const char*)a.act
                               : s == 1 ? (const char*)a.rew
                               : s == 2 ? (const char*)a.disc
                                        : (const char*)a.val;
-            glds16(arr + ((size_t)t * a.B + b0) * 4 + (lane & 1) * 16, base + 2 * L::LOGB + w * 1024);
+            glds16(arr + ((size_t)t * a.B + b0) * 4 + (lane & 1) * 16, base + L::SCO + w * 1024);
         }
         ++n;
     }
@@ -271,6 +283,17 @@ __global__ __launch_bounds__(64 * VtLayout<A>::NW, VtLayout<A>::WPS) void vtrace
     int issued = vt_issue_chunk<A, 0, NP>(a, rs, lds0, 0, T - L::TC, b0, w, lane);
     int mark = issued;  // VMEM ops issued once the chunk being waited for was queued
     const fi_vtrace_hparams hp = a.hp;
+#ifdef FI_VT_MUREG
+    // this lane's mu row of the next chunk, loaded one chunk ahead. Not counted in `issued`:
+    // they are issued before the chunk's last DMA group (the `mark` point), so they are older
+    // than every op the counted waits let stay in flight, and the B1 wait covers them
+    f32x2 mun[A / 2], mur[A / 2];
+    {
+        const f32x2* src = (const f32x2*)(a.mu + ((size_t)max(T - L::TC + tl, 0) * B + b) * A);
+#pragma unroll
+        for (int i = 0; i < A / 2; ++i) mun[i] = src[i];
+    }
+#endif
 
     float pg = 0.f, base = 0.f, ent = 0.f;
 #ifdef FI_VT_STAMPS  // timing experiment: s_memrealtime stamps of wave 0, written over vs
@@ -288,16 +311,27 @@ __global__ __launch_bounds__(64 * VtLayout<A>::NW, VtLayout<A>::WPS) void vtrace
         lds_barrier();  // B1: chunk k landed for every wave; slot (k+1)&1 fully consumed
         VT_STAMP();
         const bool more = k + 1 < nchunks;
+#ifdef FI_VT_MUREG
+#pragma unroll
+        for (int i = 0; i < A / 2; ++i) mur[i] = mun[i];
+        if (more) {
+            const f32x2* src = (const f32x2*)(a.mu + ((size_t)max(t0 - L::TC + tl, 0) * B + b) * A);
+#pragma unroll
+            for (int i = 0; i < A / 2; ++i) mun[i] = src[i];
+        }
+#endif
         if (more) issued += vt_issue_chunk<A, 0, G1>(a, rs, lds0, slot ^ 1, t0 - L::TC, b0, w, lane);
         VT_STAMP();
 #ifndef FI_VT_DMAONLY
         char* sl = smem + slot * L::SLOT;
         float* zpi = (float*)sl + tl * L::ROWF + c * A;
+#ifndef FI_VT_MUREG
         float* zmu = (float*)(sl + L::LOGB) + tl * L::ROWF + c * A;
-        const int* sact = (const int*)(sl + 2 * L::LOGB);
-        const float* srew = (const float*)(sl + 2 * L::LOGB + L::SCB);
-        const float* sdisc = (const float*)(sl + 2 * L::LOGB + 2 * L::SCB);
-        const float* sval = (const float*)(sl + 2 * L::LOGB + 3 * L::SCB);
+#endif
+        const int* sact = (const int*)(sl + L::SCO);
+        const float* srew = (const float*)(sl + L::SCO + L::SCB);
+        const float* sdisc = (const float*)(sl + L::SCO + 2 * L::SCB);
+        const float* sval = (const float*)(sl + L::SCO + 3 * L::SCB);
         const int t = t0 + tl;
         const bool valid = t >= 0;
 
@@ -308,11 +342,25 @@ __global__ __launch_bounds__(64 * VtLayout<A>::NW, VtLayout<A>::WPS) void vtrace
 #pragma unroll
         for (int i = 0; i < A / 2; ++i) {
             zp2[i] = *(const f32x2*)(zpi + 2 * i);
+#ifdef FI_VT_MUREG
+            zm2[i] = mur[i];
+#else
             zm2[i] = *(const f32x2*)(zmu + 2 * i);
+#endif
         }
         int at = sact[tl * L::NB + c];
         at = at < 0 ? 0 : (at >= A ? A - 1 : at);
+#ifdef FI_VT_MUREG
+        float zma = zm2[0].x;
+#pragma unroll
+        for (int i = 0; i < A / 2; ++i) {
+            zma = at == 2 * i ? zm2[i].x : zma;
+            zma = at == 2 * i + 1 ? zm2[i].y : zma;
+        }
+        const float zpa = zpi[at];
+#else
         const float zpa = zpi[at], zma = zmu[at];
+#endif
         const float rw = srew[tl * L::NB + c];
         const float g = sdisc[tl * L::NB + c];
         const float v = sval[tl * L::NB + c];
@@ -359,7 +407,11 @@ __global__ __launch_bounds__(64 * VtLayout<A>::NW, VtLayout<A>::WPS) void vtrace
         if (more) issued += vt_issue_chunk<A, G2, NP>(a, rs, lds0, slot ^ 1, t0 - L::TC, b0, w, lane);
         mark = issued;  // the wait for chunk k+1 ignores the stores issued after this point
         // wave total -> this wave's own first mu row (no other wave reads it)
+#ifdef FI_VT_MUREG
+        float* tot = (float*)(sl + L::SCO + 4 * L::SCB) + 16 * w;
+#else
         float* tot = (float*)(sl + L::LOGB) + (8 * w) * L::ROWF;
+#endif
         if (lane < 8) {
             tot[c] = d;
             tot[8 + c] = gg;
@@ -371,7 +423,11 @@ __global__ __launch_bounds__(64 * VtLayout<A>::NW, VtLayout<A>::WPS) void vtrace
         float carry_new = carry;
 #pragma unroll
         for (int w2 = L::NW - 1; w2 >= 0; --w2) {
+#ifdef FI_VT_MUREG
+            const float* t2 = (const float*)(sl + L::SCO + 4 * L::SCB) + 16 * w2;
+#else
             const float* t2 = (const float*)(sl + L::LOGB) + (8 * w2) * L::ROWF;
+#endif
             carry_new = t2[c] + t2[8 + c] * carry_new;
             if (w2 == w + 1) acc_in = carry_new;
         }
