@@ -259,6 +259,33 @@ __device__ __forceinline__ int vt_issue_chunk(const VtArgs& a, const VtRsrc& rs,
     return n;
 }
 
+#ifndef FI_VT_SHFLSCAN
+// v from lane ^ S, in VALU cross-lane ops (no LDS round trip): S = 8 by DPP row_ror:8 inside
+// each 16-lane row, S = 16 / 32 by gfx950's v_permlane16_swap / v_permlane32_swap
+template <int S>
+__device__ __forceinline__ float vt_xor(float v, int lane) {
+    const unsigned u = __float_as_uint(v);
+    if constexpr (S == 8) {
+        return __uint_as_float(__builtin_amdgcn_update_dpp(0u, u, 0x128, 0xf, 0xf, false));
+    } else if constexpr (S == 16) {
+        const auto q = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+        return __uint_as_float((lane & 16) ? q[0] : q[1]);
+    } else {
+        const auto q = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+        return __uint_as_float((lane & 32) ? q[0] : q[1]);
+    }
+}
+template <int S>
+__device__ __forceinline__ void vt_xscan_step(float& sd, float& sg, float& ed, float& eg, int lane) {
+    const float pd = vt_xor<S>(sd, lane), pg = vt_xor<S>(sg, lane);
+    const bool later = (lane & S) == 0;  // partner segment holds later rows
+    ed = later ? ed + eg * pd : ed;
+    eg = later ? eg * pg : eg;
+    sd = later ? sd + sg * pd : pd + pg * sd;
+    sg = sg * pg;
+}
+#endif
+
 template <int A>
 __global__ __launch_bounds__(64 * VtLayout<A>::NW, VtLayout<A>::WPS) void vtrace_lds_kernel(VtArgs a) {
     using L = VtLayout<A>;
@@ -398,12 +425,23 @@ __global__ __launch_bounds__(64 * VtLayout<A>::NW, VtLayout<A>::WPS) void vtrace
         float d = valid ? rho * (rw + g * vn - v) : 0.f;
         float gg = valid ? g * cc : 1.f;
 
+#ifndef FI_VT_SHFLSCAN
+        // butterfly over the wave's 8 rows (lane ^ 8, ^ 16, ^ 32): (sd, sg) = the composition
+        // of the lane's current row segment, (ed, eg) = the composition of the rows after this
+        // one inside it; at the end (sd, sg) is the wave total in every row
+        const float d_own = d, g_own = gg;
+        float ed = 0.f, eg = 1.f;
+        vt_xscan_step<8>(d, gg, ed, eg, lane);
+        vt_xscan_step<16>(d, gg, ed, eg, lane);
+        vt_xscan_step<32>(d, gg, ed, eg, lane);
+#else
         // inclusive suffix composition over the wave's 8 rows (lanes +8, +16, +32)
 #pragma unroll
         for (int s = 8; s < 64; s <<= 1) {
             const float d2 = __shfl_down(d, s, 64), g2 = __shfl_down(gg, s, 64);
             if (lane + s < 64) { d = d + gg * d2; gg = gg * g2; }
         }
+#endif
         if (more) issued += vt_issue_chunk<A, G2, NP>(a, rs, lds0, slot ^ 1, t0 - L::TC, b0, w, lane);
         mark = issued;  // the wait for chunk k+1 ignores the stores issued after this point
         // wave total -> this wave's own first mu row (no other wave reads it)
@@ -432,9 +470,14 @@ __global__ __launch_bounds__(64 * VtLayout<A>::NW, VtLayout<A>::WPS) void vtrace
             if (w2 == w + 1) acc_in = carry_new;
         }
         if (w == L::NW - 1) acc_in = carry;
+#ifndef FI_VT_SHFLSCAN
+        const float acc_nx = ed + eg * acc_in;
+        const float acc = d_own + g_own * acc_nx;
+#else
         const float acc = d + gg * acc_in;
         const float acc_up = __shfl_down(acc, 8, 64);
         const float acc_nx = (r == 7) ? acc_in : acc_up;
+#endif
         const float vs_t = v + acc;
         const float vs_n = vn + acc_nx;
         const float adv = pgr * (rw + g * vs_n - v);
