@@ -80,11 +80,55 @@ constexpr size_t kSinkFloats = 2048 + 2 * 20 * 1024;  // + stamps of up to 1024 
 constexpr size_t kSinkFloats = 2048;
 #endif
 
+#ifndef FI_VT_SHFLSUM
+// wave-wide double sum in VALU cross-lane moves (no ds_bpermute round trips in the
+// workgroup's tail): rotations 8, 4, 2, 1 inside each 16-lane row by DPP, then the row pairs
+// and halves by gfx950's v_permlane16_swap / v_permlane32_swap. The summation order is
+// fixed, so the result is deterministic; lane 0 holds the total the callers use.
+template <int CTRL>
+__device__ __forceinline__ double vt_dpp_d(double v) {
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = __builtin_amdgcn_update_dpp(0u, (unsigned)u, CTRL, 0xf, 0xf, false);
+    const unsigned hi = __builtin_amdgcn_update_dpp(0u, (unsigned)(u >> 32), CTRL, 0xf, 0xf, false);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+template <int S>
+__device__ __forceinline__ double vt_xor_d(double v, int lane) {
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)u, hi = (unsigned)(u >> 32);
+    unsigned rlo, rhi;
+    if constexpr (S == 16) {
+        const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+        const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+        rlo = (lane & 16) ? a[0] : a[1];
+        rhi = (lane & 16) ? b[0] : b[1];
+    } else {
+        const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+        const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+        rlo = (lane & 32) ? a[0] : a[1];
+        rhi = (lane & 32) ? b[0] : b[1];
+    }
+    return __longlong_as_double((long long)(((unsigned long long)rhi << 32) | rlo));
+}
+__device__ __forceinline__ double vt_wave_sum(double v) {
+    const int lane = threadIdx.x & 63;
+    v += vt_dpp_d<0x128>(v);  // row_ror:8
+    v += vt_dpp_d<0x124>(v);  // row_ror:4
+    v += vt_dpp_d<0x122>(v);  // row_ror:2
+    v += vt_dpp_d<0x121>(v);  // row_ror:1
+    v += vt_xor_d<16>(v, lane);
+    v += vt_xor_d<32>(v, lane);
+    return v;
+}
+#else
+__device__ __forceinline__ double vt_wave_sum(double v) { return wave_sum(v); }
+#endif
+
 __device__ __forceinline__ void block_reduce3(double pg, double base, double ent, double* red,
                                               double* out) {
-    pg = wave_sum(pg);
-    base = wave_sum(base);
-    ent = wave_sum(ent);
+    pg = vt_wave_sum(pg);
+    base = vt_wave_sum(base);
+    ent = vt_wave_sum(ent);
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (lane == 0) {
         red[w * 3 + 0] = pg;
