@@ -584,7 +584,11 @@ __global__ __launch_bounds__(64 * VtLayout<A>::NW, VtLayout<A>::WPS) void vtrace
 #endif  // FI_VT_DMAONLY
         VT_STAMP();
     }
+#ifdef FI_VT_TAILWAIT
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    // no vmcnt(0) here: the last chunk issues no LDS-DMA (only global stores are in flight),
+    // so the loss-partial reduction below can overlap the store drain
     VT_STAMP();
 #ifdef FI_VT_STAMPS
     if (tid == 0)
