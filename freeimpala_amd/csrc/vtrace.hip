@@ -429,8 +429,18 @@ __global__ __launch_bounds__(64 * VtLayout<A>::NW, VtLayout<A>::WPS) void vtrace
             zma = at == 2 * i + 1 ? zm2[i].y : zma;
         }
         const float zpa = zpi[at];
-#else
+#elif !defined(FI_VT_REGAT)
         const float zpa = zpi[at], zma = zmu[at];
+#else
+        // the taken action's logits picked from the registers (no second, dependent LDS read)
+        float zpa = zp2[0].x, zma = zm2[0].x;
+#pragma unroll
+        for (int i = 0; i < A / 2; ++i) {
+            zpa = at == 2 * i ? zp2[i].x : zpa;
+            zpa = at == 2 * i + 1 ? zp2[i].y : zpa;
+            zma = at == 2 * i ? zm2[i].x : zma;
+            zma = at == 2 * i + 1 ? zm2[i].y : zma;
+        }
 #endif
         const float rw = srew[tl * L::NB + c];
         const float g = sdisc[tl * L::NB + c];
@@ -536,8 +546,17 @@ __global__ __launch_bounds__(64 * VtLayout<A>::NW, VtLayout<A>::WPS) void vtrace
             const float al = inv * (adv - ec * (plogp + lse)), be = inv * ec;
             const f32x2 al2 = {al, al};
 #pragma unroll
+#ifndef FI_VT_REGAT
             for (int i = 0; i < A / 2; ++i) *(f32x2*)(zpi + 2 * i) = e2[i] * (zp2[i] * be + al2);
             zpi[at] -= adv;
+#else
+            for (int i = 0; i < A / 2; ++i) {  // - adv at the taken action, in registers
+                f32x2 dz = e2[i] * (zp2[i] * be + al2);
+                dz.x = at == 2 * i ? dz.x - adv : dz.x;
+                dz.y = at == 2 * i + 1 ? dz.y - adv : dz.y;
+                *(f32x2*)(zpi + 2 * i) = dz;
+            }
+#endif
         }
         if (valid) {
             pg += -adv * lpa;
