@@ -729,6 +729,8 @@ struct AtariImpl {
     bool fuse21 = true;    // conv2 backward + conv1 wgrad in one kernel (FI_BWD_UNFUSED=1 -> two)
     bool keep_da1 = false; // fused backward also stores da1 to HBM (FI_KEEP_DA1=1; parity checks)
     bool a1_planar = true; // fused fwd + bwd: a1 stored in conv21's image order (FI_A1_NHWC=1 -> NHWC)
+    int fr_grid = 256;     // persistent frame-resident workgroups, 1 per CU (FI_FR_GRID=g: tests put
+                           // many frames on each workgroup at small N to reach the steady state)
     FcBlasLt* fc = nullptr;  // fc layer GEMMs (hipBLASLt)
 };
 
@@ -750,7 +752,6 @@ int conv2_bwd_fr_launch(const __bf16* a1, const __bf16* da2, const __bf16* w2d, 
                         float* cs_slab, int nframes, int grid, hipStream_t s);
 int conv3_bwd_fr_launch(const __bf16* a2, const __bf16* da3, const __bf16* a3, const __bf16* w3d, __bf16* da2,
                         float* slab, float* cs_slab, int nframes, int grid, hipStream_t s);
-constexpr int FR_GRID = 256;  // persistent frame-resident workgroups (1 per CU)
 
 static AtariImpl* impl(AtariNet* n) { return (AtariImpl*)n->impl; }
 
@@ -785,6 +786,7 @@ AtariNet* atari_create(int B, int T, int A) {
     I->keep_da1 = std::getenv("FI_KEEP_DA1") != nullptr;
     // only conv21_bwd_fr reads a1 when both fused kernels run; every other consumer wants NHWC
     I->a1_planar = I->fr && I->fuse12 && I->fuse21 && std::getenv("FI_A1_NHWC") == nullptr;
+    if (const char* g = std::getenv("FI_FR_GRID")) I->fr_grid = std::max(1, std::min(256, std::atoi(g)));
     I->cs2 = (int)(((N * 100) + GBM - 1) / GBM * GBM);
     I->cs3 = (int)(((N * 81) + GBM - 1) / GBM * GBM);
     bool ok = dmalloc(I, &I->a1, N * 400 * 32) && dmalloc(I, &I->a2, N * 81 * 64) &&
@@ -852,10 +854,10 @@ int atari_forward(AtariNet* n, const uint8_t* frames, float* logits, float* valu
     if (I->fr && I->fuse12) {
         TagScope ts(tg, "conv12_fwd");
         rc = conv12_fwd_fr_launch(frames, I->wb.c1T, p + o.c1b, I->wb.c2T, p + o.c2b, I->a1, I->a2, N,
-                                  std::min(N, FR_GRID), s, I->a1_planar);
+                                  std::min(N, I->fr_grid), s, I->a1_planar);
     } else if (I->fr) {
         TagScope ts(tg, "conv1_fwd");
-        rc = conv1_fwd_fr_launch(frames, I->wb.c1T, p + o.c1b, I->a1, N, std::min(N, FR_GRID), s);
+        rc = conv1_fwd_fr_launch(frames, I->wb.c1T, p + o.c1b, I->a1, N, std::min(N, I->fr_grid), s);
     } else { TagScope ts(tg, "conv1_fwd"); rc = gemm<256, 32, 4, 1>(Conv1Gather{frames, N * P1}, RowsBf16{I->wb.c1T, C1O, C1K},
                              EpiAct{I->a1, C1O, p + o.c1b, 1.0f / 255.0f}, N * P1, C1O, C1K, s); }
     if (rc) return rc;
@@ -863,13 +865,13 @@ int atari_forward(AtariNet* n, const uint8_t* frames, float* logits, float* valu
         // conv2 ran inside conv12_fwd
     } else if (I->fr) {
         TagScope ts(tg, "conv2_fwd");
-        rc = conv2_fwd_fr_launch(I->a1, I->wb.c2T, p + o.c2b, I->a2, N, std::min(N, FR_GRID), s);
+        rc = conv2_fwd_fr_launch(I->a1, I->wb.c2T, p + o.c2b, I->a2, N, std::min(N, I->fr_grid), s);
     } else { TagScope ts(tg, "conv2_fwd"); rc = gemm<128, 64, 2, 2>(ConvGather<20, 32, 4, 2, 9>{I->a1, N * P2}, RowsBf16{I->wb.c2T, C2O, C2K},
                              EpiAct{I->a2, C2O, p + o.c2b, 1.0f}, N * P2, C2O, C2K, s); }
     if (rc) return rc;
     if (I->fr) {
         TagScope ts(tg, "conv3_fwd");
-        rc = conv3_fwd_fr_launch(I->a2, I->wb.c3T, p + o.c3b, I->a3, N, std::min(N, FR_GRID), s);
+        rc = conv3_fwd_fr_launch(I->a2, I->wb.c3T, p + o.c3b, I->a3, N, std::min(N, I->fr_grid), s);
     } else { TagScope ts(tg, "conv3_fwd"); rc = gemm<128, 64, 2, 2>(ConvGather<9, 64, 3, 1, 7>{I->a2, N * P3}, RowsBf16{I->wb.c3T, C3O, C3K},
                              EpiAct{I->a3, C3O, p + o.c3b, 1.0f}, N * P3, C3O, C3K, s); }
     if (rc) return rc;
@@ -915,7 +917,7 @@ int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, con
     FI_A("fc_dgrad", fc_blaslt_dgrad(I->fc, I->dh, I->wb.fcB, I->da3, s));
     // conv3: wgrad [576][64] + bias, dgrad -> da2 (masked by a2)
     if (I->fr) {
-        const int grid = std::min(N, FR_GRID);
+        const int grid = std::min(N, I->fr_grid);
         FI_A("conv3_bwd", conv3_bwd_fr_launch(I->a2, I->da3, I->a3, I->wb.c3D, I->da2, slab, cs, N, grid, s));
         FI_A("reduce_slabs", reduce_slabs(slab, grid, (size_t)C3K * C3O, grads + o.c3w, s));
         FI_A("reduce_slabs", reduce_slabs(cs, grid, (size_t)C3O, grads + o.c3b, s));
@@ -931,7 +933,7 @@ int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, con
     }
     // conv2 backward + conv1 wgrad fused: da1 stays in LDS (written to HBM only with FI_KEEP_DA1)
     if (I->fr && I->fuse21) {
-        const int grid = std::min(N, FR_GRID);
+        const int grid = std::min(N, I->fr_grid);
         float* slab1 = slab + (size_t)grid * C2K * C2O;
         float* cs1 = cs + (size_t)grid * C2O;
         FI_A("conv21_bwd", conv21_bwd_fr_launch(I->a1, I->da2, I->wb.c2D, frames, I->keep_da1 ? I->da1 : nullptr,
@@ -944,7 +946,7 @@ int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, con
     }
     // conv2: wgrad [512][64] + bias, dgrad -> da1 (4 parity classes, masked by a1)
     if (I->fr) {
-        const int grid = std::min(N, FR_GRID);
+        const int grid = std::min(N, I->fr_grid);
         FI_A("conv2_bwd", conv2_bwd_fr_launch(I->a1, I->da2, I->wb.c2D, I->da1, slab, cs, N, grid, s));
         FI_A("reduce_slabs", reduce_slabs(slab, grid, (size_t)C2K * C2O, grads + o.c2w, s));
         FI_A("reduce_slabs", reduce_slabs(cs, grid, (size_t)C2O, grads + o.c2b, s));
@@ -959,7 +961,7 @@ int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, con
     }
     // conv1: wgrad [256][32] (+1/255 input scale) + bias
     if (I->fr) {
-        const int grid = std::min(N, FR_GRID);
+        const int grid = std::min(N, I->fr_grid);
         FI_A("conv1_wgrad", conv1_wgrad_fr_launch(frames, I->da1, slab, cs, N, grid, s));
         FI_A("reduce_slabs", reduce_slabs(slab, grid, (size_t)C1K * C1O, grads + o.c1w, s));
         FI_A("reduce_slabs", reduce_slabs(cs, grid, (size_t)C1O, grads + o.c1b, s));

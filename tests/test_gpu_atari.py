@@ -41,22 +41,26 @@ def test_atari_synth_frames_bit_exact(orc):
     np.testing.assert_array_equal(L.tensor("actions", np.int32, (1, 16)), ref["actions"])
 
 
-@pytest.mark.parametrize("T,B", [(2, 16), (3, 32), (2, 7)])  # (2, 7): 21 frames, odd and ragged
-def test_atari_forward_backward_parity(orc, T, B, monkeypatch):
-    A = 18
-    monkeypatch.setenv("FI_KEEP_DA1", "1")  # the fused conv2/conv1 backward keeps da1 in LDS otherwise
-    monkeypatch.setenv("FI_A1_NHWC", "1")   # a1 in NHWC (the fused pair stores it in conv21's image order)
-    L = mk(T=T, B=B, A=A)
-    L.synth(seed=T * 100 + B)
+def _check_step_against_oracle(orc, L, T, B, A, a1_planar=False, da1=None):
+    """One resident step of L, every stage against the oracle (bf16 emulation): activations,
+    logits/values, V-trace outputs and loss (1e-5), data gradients, every weight and bias
+    gradient, and the SGD update. a1_planar: L stores a1 in conv21's image order.
+    da1: (N, 20, 20, 32) float data gradient of conv1 when L does not store it itself."""
     N = (T + 1) * B
     frames = L.tensor("frames", np.uint8, (N, 84, 84, 4))
     p0 = L.get_params()
     st = L.step_resident()
     acts = orc.atari_forward(frames, p0, A=A, bf16_emul=True)
-    for name, shape in [("a1", (N, 20, 20, 32)), ("a2", (N, 9, 9, 64)), ("a3", (N, 7, 7, 64)),
-                        ("h", (N, 512))]:
-        gpu = bf16_to_f32(L.tensor(name, np.uint16, shape))
-        rel(gpu, orc.bf16_round(acts[name]), name)
+
+    def a1_of(L_):
+        a = L_.tensor("a1", np.uint16, (N, 12800))
+        return bf16_to_f32(a1_planar_to_nhwc(a) if a1_planar else a.reshape(N, 20, 20, 32))
+
+    gpu_acts = {"a1": a1_of(L)}
+    gpu_acts.update({nm: bf16_to_f32(L.tensor(nm, np.uint16, sh)) for nm, sh in
+                     [("a2", (N, 9, 9, 64)), ("a3", (N, 7, 7, 64)), ("h", (N, 512))]})
+    for name in ("a1", "a2", "a3", "h"):
+        rel(gpu_acts[name], orc.bf16_round(acts[name]), name)
     logits = L.tensor("logits", shape=(T + 1, B, A))
     values = L.tensor("values", shape=(T + 1, B))
     rel(logits.reshape(N, A), acts["out"][:, :A], "logits")
@@ -78,13 +82,12 @@ def test_atari_forward_backward_parity(orc, T, B, monkeypatch):
     dout = np.zeros((N, A + 1), np.float32)
     dout[:T * B, :A] = dl.reshape(T * B, A)
     dout[:, A] = dv.reshape(N)
-    gpu_acts = {nm: bf16_to_f32(L.tensor(nm, np.uint16, sh)) for nm, sh in
-                [("a1", (N, 20, 20, 32)), ("a2", (N, 9, 9, 64)), ("a3", (N, 7, 7, 64)), ("h", (N, 512))]}
     g_ref, mids = orc.atari_backward_ex(frames, p0, gpu_acts, dout, A=A, bf16_emul=True)
     # da3 is stored before its ReLU mask (the fc dgrad is a plain library GEMM; conv3's
     # backward applies (a3 > 0) as it loads da3), so mask it here
     dev = {nm: bf16_to_f32(L.tensor(nm, np.uint16, sh)) for nm, sh in
-           [("dh", (N, 512)), ("da3", (N, 7, 7, 64)), ("da2", (N, 9, 9, 64)), ("da1", (N, 20, 20, 32))]}
+           [("dh", (N, 512)), ("da3", (N, 7, 7, 64)), ("da2", (N, 9, 9, 64))]}
+    dev["da1"] = bf16_to_f32(L.tensor("da1", np.uint16, (N, 20, 20, 32))) if da1 is None else da1
     dev["da3"] = dev["da3"] * (gpu_acts["a3"] > 0)
     for nm, key in [("dh", "dh"), ("da3", "d3"), ("da2", "d2"), ("da1", "d1")]:
         rel(dev[nm], orc.bf16_round(mids[key]), nm)
@@ -108,6 +111,49 @@ def test_atari_forward_backward_parity(orc, T, B, monkeypatch):
     rel(g[off[9]:off[10]], dout.astype(np.float64).sum(0), "hb", l2=1e-5, mx=1e-4)
     # SGD update uses exactly the gradient the kernels produced
     np.testing.assert_allclose(L.get_params(), p0 - np.float32(1e-3) * g, rtol=0, atol=1e-6)
+    return g
+
+
+@pytest.mark.parametrize("T,B", [(2, 16), (3, 32), (2, 7)])  # (2, 7): 21 frames, odd and ragged
+def test_atari_forward_backward_parity(orc, T, B, monkeypatch):
+    A = 18
+    monkeypatch.setenv("FI_KEEP_DA1", "1")  # the fused conv2/conv1 backward keeps da1 in LDS otherwise
+    monkeypatch.setenv("FI_A1_NHWC", "1")   # a1 in NHWC (the fused pair stores it in conv21's image order)
+    L = mk(T=T, B=B, A=A)
+    L.synth(seed=T * 100 + B)
+    _check_step_against_oracle(orc, L, T, B, A)
+    L.close()
+
+
+@pytest.mark.parametrize("T,B,grid", [(3, 32, 8), (3, 32, 3), (2, 7, 4)])
+def test_atari_production_path_steady_state_parity(orc, T, B, grid, monkeypatch):
+    """The production Atari path -- fused conv12_fwd / conv21_bwd, a1 in conv21's planar image
+    order, da1 never written to HBM -- with FI_FR_GRID shrinking the persistent grid so every
+    workgroup walks many frames (128 frames on 8 workgroups: 16 each; on 3: 42-43 each; 21
+    ragged frames on 4: 5-6 each). That exercises the LDS-DMA ring reuse, the counted vmcnt
+    waits across frames and the per-workgroup slab accumulation over frames, and every
+    gradient is compared with the oracle. A twin learner with the optional da1 store (same
+    grid) must give bit-identical gradients; its da1 is checked against the oracle and feeds
+    the c1b column-sum check."""
+    A = 18
+    monkeypatch.delenv("FI_KEEP_DA1", raising=False)
+    monkeypatch.delenv("FI_A1_NHWC", raising=False)
+    monkeypatch.delenv("FI_FWD_UNFUSED", raising=False)
+    monkeypatch.delenv("FI_BWD_UNFUSED", raising=False)
+    monkeypatch.setenv("FI_FR_GRID", str(grid))
+    N = (T + 1) * B
+    monkeypatch.setenv("FI_KEEP_DA1", "1")
+    twin = mk(T=T, B=B, A=A, seed=17)
+    monkeypatch.delenv("FI_KEEP_DA1")
+    L = mk(T=T, B=B, A=A, seed=17)
+    for x in (twin, L):
+        x.synth(seed=T * 1000 + B + grid)
+    twin.step_resident()
+    da1 = bf16_to_f32(twin.tensor("da1", np.uint16, (N, 20, 20, 32)))
+    g = _check_step_against_oracle(orc, L, T, B, A, a1_planar=True, da1=da1)
+    np.testing.assert_array_equal(g, twin.tensor("grads"))
+    twin.close()
+    L.close()
 
 
 def test_atari_training_reduces_loss():
