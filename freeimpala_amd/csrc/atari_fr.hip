@@ -1060,11 +1060,7 @@ __device__ __forceinline__ void c2_frames(const C2Ctx& c, char* smem, int nst, W
     const uint32_t lds0 = lds_addr(smem);
     // per-unit source offsets of both gathers (FI_OOB for border / gap units)
     uint32_t* tab = (uint32_t*)(smem + c2::RING * c2::SLOT);
-#ifdef FI_EXP_LINDMA  // timing experiment: coalesced linear sources (wrong results)
-    for (int i = tid; i < c2::SLOT / 16; i += 512) tab[i] = i < c2::XB / 16 ? 16 * i : (16 * (i - c2::XB / 16) < 10368 ? 16 * (i - c2::XB / 16) : FI_OOB);
-#else
     for (int i = tid; i < c2::SLOT / 16; i += 512) tab[i] = i < c2::XB / 16 ? c2_x_src(i) : c2_dy_src(i - c2::XB / 16);
-#endif
     __syncthreads();
     const int npw = w == 0 ? 11 : (w < 4 ? 10 : 0);  // pieces per wave
     const int nmine = c.nframes > (int)blockIdx.x ? (c.nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
@@ -1072,9 +1068,7 @@ __device__ __forceinline__ void c2_frames(const C2Ctx& c, char* smem, int nst, W
     ST();
     int issued = 0, m0 = 0, m1 = 0;
     for (int i = 0; i < 2 && i < nmine; ++i) {
-#ifndef FI_EXP_NODATA
         if (w < 4) c2_issue(c, tab, blockIdx.x + i * gridDim.x, lds0 + i * c2::SLOT, w, lane);
-#endif
         issued += npw;
         if (i == 0) m0 = issued; else m1 = issued;
     }
@@ -1089,16 +1083,12 @@ __device__ __forceinline__ void c2_frames(const C2Ctx& c, char* smem, int nst, W
         if (it < 5) ST();
         int m2 = 0;
         if (it + 2 < nmine) {
-#ifndef FI_EXP_NODATA
             if (w < 4) c2_issue(c, tab, f + 2 * gridDim.x, lds0 + ((it + 2) % 3) * c2::SLOT, w, lane);
-#endif
             issued += npw;
             m2 = issued;
         }
         PH(2);
-#ifndef FI_EXP_NOWORK
         work(smem + (it % 3) * c2::SLOT, f);
-#endif
         PH(3);
         PH_ITER();
         issued += nst;
@@ -1219,11 +1209,7 @@ __global__ __launch_bounds__(512, 2) void conv2_bwd_fr(const __bf16* __restrict_
         const int si = (lane & 15) ^ (((lane & 15) >> 1) & 4);
         const int bd0 = c2::XB + 16 * (si + 128 * g + c2::zc(g));
         const int bd6 = c2::XB + 16 * (min(96 + si, 99) + 128 * g + c2::zc(g));
-#ifdef FI_EXP_NODX  // timing experiment: no dX stores (wrong results)
-        c2_frames(ctx, smem, 0, [&](const char* X, int f) {
-#else
         c2_frames(ctx, smem, 7, [&](const char* X, int f) {
-#endif
             // pixel tile outer: each tile's 16 MFMAs (two accumulator chains; 16x16x32 chains
             // issue back to back) end in its own masked 16-byte store, so the dX stores spread
             // over the frame instead of queueing as a burst. The next tile's 8 fragments are
@@ -1267,13 +1253,7 @@ __global__ __launch_bounds__(512, 2) void conv2_bwd_fr(const __bf16* __restrict_
                         o[r] = m[r] > 0 ? (__bf16)acc0[r] : (__bf16)0.f;
                         o[4 + r] = m[4 + r] > 0 ? (__bf16)acc1[r] : (__bf16)0.f;
                     }
-#if defined(FI_EXP_LINDX)  // timing experiment: same stores, contiguous 1 KiB per instruction
-                    FI_ST16(__builtin_bit_cast(u32x4, o), dst + ((wr * 7 + pt) * 64 + lane) % 1600);
-#elif !defined(FI_EXP_NODX)
                     FI_ST16(__builtin_bit_cast(u32x4, o), dst + 4 * pix + g);
-#else
-                    if (o[0] == (__bf16)1234.f) *(volatile int*)dst = pix;
-#endif
                 }
             }
         });
@@ -1348,14 +1328,10 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
     const int g = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3, h = lane >> 5, col = lane & 31;
     const uint32_t lds0 = lds_addr(smem);
     uint32_t* tab = (uint32_t*)(smem + c21::O_TAB);
-#ifdef FI_EXP_LINDMA21  // timing experiment: coalesced linear DMA sources (wrong results)
-    for (int i = tid; i < (c2::XB + c2::DYB) / 16; i += 512) tab[i] = i < c2::XB / 16 ? 16 * i : (16 * (i - c2::XB / 16) < 10368 ? 16 * (i - c2::XB / 16) : FI_OOB);
-#else
     // a1 planar (conv12_fwd_fr wrote it in this image's order): the a1 pieces are linear 1-KiB
     // runs; NHWC: 16-byte gathers at a 128-byte stride
     for (int i = tid; i < (c2::XB + c2::DYB) / 16; i += 512)
         tab[i] = i < c2::XB / 16 ? (a1_planar ? 16u * i : c2_x_src(i)) : c2_dy_src(i - c2::XB / 16);
-#endif
     char* DY = smem + c21::O_DY;
     char* IMG = smem + c21::O_IMG;
     char* D = smem + c21::O_D;
@@ -1530,7 +1506,6 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                     *(bf16x8*)(IMG + c1::PLANE + 16 * u) = hi;
                 }
             }
-#if !defined(FI_EXP_NORAW) && !defined(FI_C21_RAW_LATE)  // NORAW: timing experiment, raw frame loaded once (wrong results)
             // raw(it + 1) goes out now, while this wave waits at B2 for the data-gradient
             // waves: in phase 2 its issue would queue behind the DMA (several thousand clocks
             // of issue stall per frame with both there)
@@ -1538,23 +1513,14 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                 load_raw(it + 1);
                 issued += c21::NRAW_A;
             }
-#endif
             PH(3);
             lds_barrier();  // B2: D and the image complete; da2 image and a1 slot it&1 consumed
             PH(1);
-#ifndef FI_EXP_NOISSUE2  // timing experiment: no DMA after frame 0 (wrong results)
             if (it + 1 < nmine) {
                 issued += issue_dy(it + 1);
                 m_dy = issued;
             }
             if (it + 2 < nmine) issued += issue_ax(it + 2, it & 1);
-#endif
-#ifdef FI_C21_RAW_LATE  // A/B: raw(it + 1) loaded after the phase-2 DMA issue
-            if (it + 1 < nmine) {
-                load_raw(it + 1);
-                issued += c21::NRAW_A;
-            }
-#endif
             PH(4);
             PH_ITER();
         }
@@ -1642,9 +1608,7 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                             o[4 + r] = m[4 + r] > 0 ? (__bf16)e1[r] : (__bf16)0.f;
                         }
                         const u32x4 ov = __builtin_bit_cast(u32x4, o);
-#ifndef FI_EXP_NODW  // timing experiment: no da1 tile writes (wrong results)
                         *(u32x4*)(D + dsw(pix, g)) = ov;
-#endif
 #pragma unroll
                         for (int j = 0; j < 8; ++j) bs8[j] += (float)o[j];
                         if constexpr (KEEP_DA1) FI_ST16(ov, dst + 4 * pix + g);
@@ -1793,72 +1757,6 @@ __device__ __forceinline__ void c3_issue(const C3Ctx& c, const uint32_t* tab, in
     }
 }
 
-#ifdef FI_C3_GATHER  // A/B: the gathered-DMA pipeline (3-slot ring, chunk-planar images DMA'd directly)
-namespace c3 {
-constexpr int LDS = RING * SLOT + (XB + DYB) / 16 * 4;
-}  // namespace c3
-// one barrier per frame (see c2_frames); the issuing waves mask their own dY pieces first
-template <bool ISSUER, class Work>
-__device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, int nst, Work&& work) {
-    const int lane = threadIdx.x & 63, w = wave_id(), tid = threadIdx.x;
-    const uint32_t lds0 = lds_addr(smem);
-    uint32_t* tab = (uint32_t*)(smem + c3::RING * c3::SLOT);
-#ifdef FI_EXP_LINDMA
-    for (int i = tid; i < (c3::XB + c3::DYB) / 16; i += 512) tab[i] = i < c3::XB / 16 ? (16 * i < 10368 ? 16 * i : FI_OOB) : (16 * (i - c3::XB / 16) < 6272 ? 16 * (i - c3::XB / 16) : FI_OOB);
-#else
-    for (int i = tid; i < (c3::XB + c3::DYB) / 16; i += 512) tab[i] = i < c3::XB / 16 ? c3_x_src(i) : c3_dy_src(i - c3::XB / 16);
-#endif
-    __syncthreads();
-    const int npw = w < 4 ? 11 : 0;
-    const int nmine = c.nframes > (int)blockIdx.x ? (c.nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
-    int issued = 0, m0 = 0, m1 = 0;
-    for (int i = 0; i < 2 && i < nmine; ++i) {
-        if (w < 4) c3_issue(c, tab, blockIdx.x + i * gridDim.x, lds0 + i * c3::SLOT, w, lane);
-        issued += npw;
-        if (i == 0) m0 = issued; else m1 = issued;
-    }
-    PH_DECL
-    for (int it = 0; it < nmine; ++it) {
-        const int f = blockIdx.x + it * gridDim.x;
-        char* X = smem + (it % 3) * c3::SLOT;
-        PH(5);
-        if (w < 4) {
-            wait_vmcnt(issued - m0);
-            // dY *= (a3 > 0) on this wave's own pieces (units 64(w + 4i) + lane)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                s16x8* dyp = (s16x8*)(X + c3::XB + 16 * (64 * (w + 4 * i) + lane));
-                const s16x8 m = *(const s16x8*)((const char*)dyp + c3::DYB);
-                s16x8 v = *dyp;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) v[j] = m[j] > 0 ? v[j] : (short)0;
-                *dyp = v;
-            }
-        }
-        PH(0);
-        lds_barrier();  // frame it landed and masked; frame it-1 consumed by every wave
-        PH(1);
-        int m2 = 0;
-        if (it + 2 < nmine) {
-            if (w < 4) c3_issue(c, tab, f + 2 * gridDim.x, lds0 + ((it + 2) % 3) * c3::SLOT, w, lane);
-            issued += npw;
-            m2 = issued;
-        }
-        PH(2);
-#ifndef FI_EXP_NOWORK3  // timing experiment: data movement only (wrong results)
-        work(X, f);
-#endif
-        issued += nst;
-        PH(3);
-        PH_ITER();
-        m0 = m1;
-        m1 = m2;
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    PH_FLUSH();
-}
-
-#else
 // Linear-DMA pipeline: every frame's a2, da3 and a3 arrive by LDS-DMA in their own byte order
 // (1 KiB contiguous per wave instruction) into one of two staging buffers; the issuing wave
 // then moves its own landed pieces into the frame's image slot (chunk-planar X, bordered dY),
@@ -1992,9 +1890,7 @@ __device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, int nst, W
             mB = mC;
         }
         PH(2);
-#ifndef FI_EXP_NOWORK3  // timing experiment: data movement only (wrong results)
         work(X, f);
-#endif
         issued += nst;
         PH(3);
         PH_ITER();
@@ -2002,7 +1898,6 @@ __device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, int nst, W
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     PH_FLUSH();
 }
-#endif
 
 // weight gradient of one wave, taps t = 2i + B (B = wr>>1), i < 5 - B
 template <int B>
@@ -2170,21 +2065,11 @@ __global__ __launch_bounds__(512, 2) void conv3_bwd_fr(const __bf16* __restrict_
                         o[r] = m[r] > 0 ? (__bf16)acc[ti][0][r] : (__bf16)0.f;
                         o[4 + r] = m[4 + r] > 0 ? (__bf16)acc[ti][1][r] : (__bf16)0.f;
                     }
-#if defined(FI_EXP_LINDX)
-                    FI_ST16(__builtin_bit_cast(u32x4, o), dst + ((wr * 3 + ti) * 64 + lane) % 648);
-#elif !defined(FI_EXP_NODX)
                     FI_ST16(__builtin_bit_cast(u32x4, o), dst + 8 * ri + c);
-#else
-                    if (o[0] == (__bf16)1234.f) *(volatile int*)dst = ri;
-#endif
                 }
             }
         };
-#ifdef FI_EXP_NODX
-        c3_frames<false>(ctx, smem, 0, [&](const char* X, int f) {
-#else
         c3_frames<false>(ctx, smem, 3, [&](const char* X, int f) {
-#endif
             if (ph) work(std::integral_constant<int, 1>{}, X, f);
             else work(std::integral_constant<int, 0>{}, X, f);
         });

@@ -23,8 +23,11 @@ int vtrace_launch(int variant, int T, int B, int A, const float* pi, const float
                   const int32_t* act, const float* rew, const float* disc, const float* val,
                   const fi_vtrace_hparams& hp, float* vs, float* adv, float* dlog, float* dval,
                   double* losses, void* ws, size_t ws_bytes, hipStream_t stream,
-                  bool finalize = true, int* nblk_out = nullptr);
-int vtrace_finalize_launch(void* ws, int nblk, double* losses, hipStream_t stream);
+                  bool finalize = true, int* nblk_out = nullptr, int* bad = nullptr);
+// bad: device counter of out-of-range actions (nullptr: a counter inside ws, zeroed here; with
+// finalize the loss scalars become NaN when it is non-zero)
+int vtrace_finalize_launch(void* ws, int nblk, double* losses, hipStream_t stream,
+                           const int* bad = nullptr);
 // per-workgroup loss partials [nblk][3] inside a vtrace workspace
 const double* vtrace_partials(const void* ws);
 
@@ -52,13 +55,14 @@ int grad_sqnorm(const float* g, size_t n, double* part, int nblk, double* out, h
                 const double* vt_part = nullptr, int vt_nblk = 0, double* vt_losses = nullptr);
 int optimizer_step(int opt, float* p, const float* g, float* m, float* v, size_t n, float lr,
                    float b1, float b2, float eps, double bc1, double bc2, const double* sqnorm,
-                   float max_norm, hipStream_t s);
+                   float max_norm, hipStream_t s, const int* skip = nullptr);
 int to_bf16(const float* src, uint16_t* dst, size_t n, hipStream_t s);
 int fill_hash_bf16(void* dst, size_t n, uint32_t seed, hipStream_t s);
 int synth_launch(uint64_t seed, int T, int B, int B_glob, int b_off, int A, int D, float gamma,
                  float* obs, float* mu, int32_t* act, float* rew, float* disc, uint8_t* frames,
                  hipStream_t s);
+// actions outside [0, A) are counted into *bad (nullable) and stored clamped
 int ingest_launch(const void* rec, int T, int B, int A, int D, size_t entry_bytes, float* obs,
-                  float* mu, int32_t* act, float* rew, float* disc, hipStream_t s);
+                  float* mu, int32_t* act, float* rew, float* disc, hipStream_t s, int* bad = nullptr);
 
 }  // namespace fi

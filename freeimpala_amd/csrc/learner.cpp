@@ -70,6 +70,7 @@ struct fi_learner {
     float* dlogits = nullptr;
     float* dvalue = nullptr;
     double* small = nullptr;  // [0..2] losses, [3] grad sqnorm, [8..] sqnorm partials
+    int* bad = nullptr;       // actions outside [0, A) in the current step's batch
     void* vt_ws = nullptr;
     size_t vt_ws_bytes = 0;
     float* slab = nullptr;
@@ -296,6 +297,8 @@ static int create(const fi_learner_config* cfg, fi_learner** out) {
     FI_TRY(dalloc_n(l, &l->dlogits, TB * A));
     FI_TRY(dalloc_n(l, &l->dvalue, rows));
     FI_TRY(dalloc_n(l, &l->small, 8 + kSqParts));
+    FI_TRY(dalloc_n(l, &l->bad, 64));
+    FI_HIP_CHECK(hipMemsetAsync(l->bad, 0, 64 * sizeof(int), l->stream));
     l->vt_ws_bytes = vtrace_workspace_bytes(l->T, l->B, A);
     FI_TRY(dalloc(l, &l->vt_ws, l->vt_ws_bytes));
 
@@ -446,11 +449,42 @@ static int mlp_backward(fi_learner* l) {
     return FI_OK;
 }
 
+// A batch with actions outside [0, A) (a corrupt record, or actors configured with another
+// --num-actions) is rejected: the optimizer kernels see the device counter and leave the
+// parameters and moments untouched, and the step reports FI_ERR_INVALID once it has
+// completed (the oracle rejects the same batch, oracle/impala_oracle.c). Called after the
+// stream has been synchronised.
+static int check_rejected(fi_learner* l) {
+    int bad = 0;
+    FI_HIP_CHECK(hipMemcpy(&bad, l->bad, sizeof(int), hipMemcpyDeviceToHost));
+    if (bad == 0) return FI_OK;
+    l->step_count--;
+    l->version--;
+    return fail(FI_ERR_INVALID, "step: " + std::to_string(bad) + " action(s) outside [0, " +
+                                    std::to_string(l->A) + ") in the batch; batch rejected, "
+                                    "parameters unchanged");
+}
+
+static void fill_stats(fi_learner* l, fi_step_stats* out) {
+    double h[4];
+    if (hipMemcpy(h, l->small, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess)
+        for (double& x : h) x = std::nan("");
+    const fi_vtrace_hparams& hp = l->cfg.hp;
+    out->pg_loss = h[0];
+    out->baseline_loss = h[1];
+    out->entropy_loss = h[2];
+    out->total_loss = h[0] + hp.baseline_cost * h[1] + hp.entropy_cost * h[2];
+    out->grad_norm = std::sqrt(h[3]);
+    out->version = l->version;
+    out->step_ms = 0.f;
+}
+
 static int run_step(fi_learner* l, bool have_host_batch, fi_step_stats* out) {
     const bool sync = out != nullptr || l->profiling;
     l->tag_used = 0;
     if (out) FI_HIP_CHECK(hipEventRecord(l->ev_a, l->stream));
     mark(l, FI_PHASE_INGEST);
+    FI_HIP_CHECK(hipMemsetAsync(l->bad, 0, sizeof(int), l->stream));
     if (have_host_batch) {
         const int s = l->cur;
         FI_HIP_CHECK(hipStreamWaitEvent(l->stream, l->h2d_done[s], 0));
@@ -458,7 +492,7 @@ static int run_step(fi_learner* l, bool have_host_batch, fi_step_stats* out) {
             Tag t(l, "ingest");
             FI_TRY(ingest_launch(l->rec_slot[s], l->T, l->B, l->A, l->D, l->rec_entry_bytes,
                                  l->cfg.arch == FI_ARCH_MLP ? l->obs : nullptr, l->mu, l->act,
-                                 l->rew, l->disc, l->stream));
+                                 l->rew, l->disc, l->stream, l->bad));
         }
         FI_HIP_CHECK(hipEventRecord(l->ingest_done[s], l->stream));
     }
@@ -475,7 +509,8 @@ static int run_step(fi_learner* l, bool have_host_batch, fi_step_stats* out) {
         Tag t(l, "vtrace");
         FI_TRY(vtrace_launch(0, l->T, l->B, l->A, l->logits, l->mu, l->act, l->rew, l->disc,
                              l->values, l->cfg.hp, l->vs, l->pg_adv, l->dlogits, l->dvalue,
-                             l->small, l->vt_ws, l->vt_ws_bytes, l->stream, false, &vt_nblk));
+                             l->small, l->vt_ws, l->vt_ws_bytes, l->stream, false, &vt_nblk,
+                             l->bad));
     }
     mark(l, FI_PHASE_BACKWARD);
     if (l->cfg.arch == FI_ARCH_MLP) FI_TRY(mlp_backward(l));
@@ -505,7 +540,7 @@ static int run_step(fi_learner* l, bool have_host_batch, fi_step_stats* out) {
         Tag t(l, "optimizer");
         FI_TRY(optimizer_step(l->cfg.optimizer, l->params, l->grads, l->opt_m, l->opt_v, l->nparams,
                               l->cfg.lr, l->cfg.beta1, l->cfg.beta2, l->cfg.eps, bc1, bc2,
-                              l->small + 3, l->cfg.max_grad_norm, l->stream));
+                              l->small + 3, l->cfg.max_grad_norm, l->stream, l->bad));
     }
     if (l->atari) {
         Tag t(l, "weights_bf16");
@@ -528,15 +563,8 @@ static int run_step(fi_learner* l, bool have_host_batch, fi_step_stats* out) {
         }
     }
     if (out) {
-        double h[4];
-        FI_HIP_CHECK(hipMemcpy(h, l->small, sizeof(h), hipMemcpyDeviceToHost));
-        const fi_vtrace_hparams& hp = l->cfg.hp;
-        out->pg_loss = h[0];
-        out->baseline_loss = h[1];
-        out->entropy_loss = h[2];
-        out->total_loss = h[0] + hp.baseline_cost * h[1] + hp.entropy_cost * h[2];
-        out->grad_norm = std::sqrt(h[3]);
-        out->version = l->version;
+        FI_TRY(check_rejected(l));
+        fill_stats(l, out);
         float ms = 0.f;
         FI_HIP_CHECK(hipEventElapsedTime(&ms, l->ev_a, l->ev_b));
         out->step_ms = ms;
@@ -670,7 +698,10 @@ static int stage_entries(fi_learner* l, const void* const* entries, size_t n_ent
 static int step_and_wait(fi_learner* l, fi_step_stats* out) {
     l->in_flight = false;
     FI_TRY(run_step(l, true, out));
-    if (!out) FI_HIP_CHECK(hipStreamSynchronize(l->stream));
+    if (!out) {
+        FI_HIP_CHECK(hipStreamSynchronize(l->stream));
+        FI_TRY(check_rejected(l));
+    }
     return FI_OK;
 }
 
@@ -738,19 +769,10 @@ extern "C" int fi_learner_wait(fi_learner* l, fi_step_stats* out) {
     FI_REQUIRE(l, "wait: null learner");
     FI_HIP_CHECK(hipSetDevice(l->dev));
     FI_HIP_CHECK(hipStreamSynchronize(l->stream));
+    const bool was_in_flight = l->in_flight;
     l->in_flight = false;
-    if (out) {
-        double h[4];
-        FI_HIP_CHECK(hipMemcpy(h, l->small, sizeof(h), hipMemcpyDeviceToHost));
-        const fi_vtrace_hparams& hp = l->cfg.hp;
-        out->pg_loss = h[0];
-        out->baseline_loss = h[1];
-        out->entropy_loss = h[2];
-        out->total_loss = h[0] + hp.baseline_cost * h[1] + hp.entropy_cost * h[2];
-        out->grad_norm = std::sqrt(h[3]);
-        out->version = l->version;
-        out->step_ms = 0.f;  // not timed on the asynchronous path
-    }
+    if (was_in_flight) FI_TRY(check_rejected(l));
+    if (out) fill_stats(l, out);  // step_ms = 0: not timed on the asynchronous path
     return FI_OK;
 }
 

@@ -129,13 +129,15 @@ __global__ void ingest_vec_kernel(const char* __restrict__ rec, int rows, int B,
 }
 
 __global__ void ingest_scalar_kernel(const char* __restrict__ rec, int T, int B, int A,
-                                     size_t entry_bytes, int32_t* act, float* rew, float* disc) {
+                                     size_t entry_bytes, int32_t* act, float* rew, float* disc,
+                                     int* bad) {
     const size_t n = (size_t)T * B;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
          i += (size_t)gridDim.x * blockDim.x) {
         const int t = (int)(i / B), b = (int)(i - (size_t)t * B);
         const char* r = rec + (size_t)b * entry_bytes + (size_t)t * FI_RECORD_BYTES;
         int32_t a = *(const int32_t*)(r + REC_ACT);
+        if ((unsigned)a >= (unsigned)A && bad) atomicAdd(bad, 1);
         act[i] = a < 0 ? 0 : (a >= A ? A - 1 : a);
         rew[i] = *(const float*)(r + REC_REW);
         disc[i] = *(const float*)(r + REC_DISC);
@@ -143,7 +145,7 @@ __global__ void ingest_scalar_kernel(const char* __restrict__ rec, int T, int B,
 }
 
 int ingest_launch(const void* rec, int T, int B, int A, int D, size_t entry_bytes, float* obs,
-                  float* mu, int32_t* act, float* rew, float* disc, hipStream_t s) {
+                  float* mu, int32_t* act, float* rew, float* disc, hipStream_t s, int* bad) {
     FI_REQUIRE(rec && T >= 1 && B >= 1 && A >= 1 && A <= 64 && D <= 128, "ingest: bad shape");
     FI_REQUIRE(entry_bytes >= (size_t)(T + 1) * FI_RECORD_BYTES, "ingest: entry too small");
     const char* r = (const char*)rec;
@@ -155,7 +157,7 @@ int ingest_launch(const void* rec, int T, int B, int A, int D, size_t entry_byte
                            B, A, REC_MU, entry_bytes, mu);
     if (act && rew && disc)
         hipLaunchKernelGGL(ingest_scalar_kernel, dim3(grid_for((size_t)T * B)), dim3(256), 0, s, r, T,
-                           B, A, entry_bytes, act, rew, disc);
+                           B, A, entry_bytes, act, rew, disc, bad);
     FI_HIP_CHECK(hipGetLastError());
     return FI_OK;
 }
@@ -319,7 +321,8 @@ int grad_sqnorm(const float* g, size_t n, double* part, int nblk, double* out, h
 __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                             float* __restrict__ m, float* __restrict__ v, size_t n, float lr,
                             float b1, float b2, float eps, double bc1, double bc2,
-                            const double* sqnorm, float max_norm) {
+                            const double* sqnorm, float max_norm, const int* skip) {
+    if (skip && *skip != 0) return;  // rejected batch: parameters and moments stay as they are
     float scale = 1.f;
     if (max_norm > 0.f) {
         const double norm = sqrt(*sqnorm);
@@ -338,7 +341,8 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
 }
 
 __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, size_t n, float lr,
-                           const double* sqnorm, float max_norm) {
+                           const double* sqnorm, float max_norm, const int* skip) {
+    if (skip && *skip != 0) return;
     float scale = 1.f;
     if (max_norm > 0.f) {
         const double norm = sqrt(*sqnorm);
@@ -351,13 +355,13 @@ __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, s
 
 int optimizer_step(int opt, float* p, const float* g, float* m, float* v, size_t n, float lr,
                    float b1, float b2, float eps, double bc1, double bc2, const double* sqnorm,
-                   float max_norm, hipStream_t s) {
+                   float max_norm, hipStream_t s, const int* skip) {
     if (opt == FI_OPT_ADAM)
         hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, s, p, g, m, v, n, lr, b1,
-                           b2, eps, bc1, bc2, sqnorm, max_norm);
+                           b2, eps, bc1, bc2, sqnorm, max_norm, skip);
     else
         hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n)), dim3(256), 0, s, p, g, n, lr, sqnorm,
-                           max_norm);
+                           max_norm, skip);
     FI_HIP_CHECK(hipGetLastError());
     return FI_OK;
 }

@@ -8,17 +8,22 @@
 //   pg_adv_t = min(pg_rho_bar, e^log_rho)(r_t + g_t vs_{t+1} - V_t)
 //   dL/dz = -pg_adv (onehot - pi) + ec pi (log pi - sum pi log pi);  dL/dV_t = bc (V_t - vs_t)
 //
-// Kernel 1 (vtrace_lds_kernel, the hot one): one 256-thread workgroup owns 16 batch
-// columns for all T and walks time BACKWARDS in chunks of 16 steps. Each chunk's
-// (16 t x 16 b) slices of pi/mu logits and of the action/reward/discount/value rows are
-// contiguous 1 KiB-multiples in the (T,B,A)/(T,B) layouts, so they are staged into LDS
-// with LDS-DMA (global_load_lds_dwordx4), three chunks in flight in a ring, counted vmcnt
-// and raw s_barrier (no vmcnt(0) drains). Thread (tl, c) = (4*wave + lane/16, lane%16)
-// reads its logits row conflict-free, computes the log-softmaxes, and the reverse-time
-// affine recurrence acc_t = d_t + g_t acc_{t+1} is solved with a 2-step wavefront
-// shuffle suffix scan over the 4 timesteps of a wave plus a 4-entry LDS combine across
-// waves and a carried value across chunks. dlogits go back through LDS and leave as
-// coalesced 16-byte stores. Algorithmic HBM traffic: 12A+28 bytes per (t,b).
+// Kernel 1 (vtrace_lds_kernel<A>, the hot one): one 256-thread workgroup (4 waves) owns
+// 8 batch columns for all T and walks time BACKWARDS in chunks of 32 steps; wave w owns
+// rows 8w..8w+7 of a chunk (lane = 8*row + column). Each chunk's pi/mu logits tiles
+// (32 rows x 8 columns x A floats) and the action/reward/discount/value tiles are
+// contiguous pieces of the (T,B,A)/(T,B) layouts and arrive by LDS-DMA
+// (buffer_load_dwordx4 ... lds) into a 2-slot ring (81,920 B at A=18, two workgroups per
+// CU); the next chunk is issued right after the landing barrier, with counted vmcnt waits.
+// Per element: packed-fp32 softmax statistics, one v_exp_f32 per logit. The reverse
+// recurrence acc_t = d_t + g_t c_t acc_{t+1} is an affine suffix scan: a 3-step butterfly
+// inside the wave (DPP row_ror:8, v_permlane16_swap, v_permlane32_swap: no LDS round trip),
+// a 4-entry combine across waves through LDS and a carry kept in registers across chunks.
+// dlogits are written over the wave's own pi rows in LDS and leave as full-wave 16-byte
+// stores; the loss partials are reduced in-wave by DPP/permlane and written per workgroup
+// (summed in a fixed order by the grad-norm kernel). Algorithmic HBM traffic: 12A+28 bytes
+// per (t,b). Requires B % 8 == 0, A in {2..64 compiled set} and T*B*A*4 < 2^31 (32-bit
+// buffer offsets; vtrace_launch falls back to kernel 2 above that).
 //
 // Kernel 2 (vtrace_column_kernel): one lane per column, serial over t; any A <= 64, any B.
 #include "fi_common.h"
@@ -29,17 +34,10 @@
 
 namespace fi {
 
-#ifdef FI_VT_NOMATH  // timing experiment only: transcendental-free stand-ins
-#define VT_EXP(x) ((x) * 0.5f + 1.f)
-#define VT_LOG(x) ((x) * 0.5f)
-#define VT_EXP2(x) ((x) * 0.5f + 1.f)
-#define VT_LOG2(x) ((x) * 0.5f)
-#else
 #define VT_EXP(x) __expf(x)
 #define VT_LOG(x) __logf(x)
 #define VT_EXP2(x) __builtin_amdgcn_exp2f(x)
 #define VT_LOG2(x) __builtin_amdgcn_logf(x)
-#endif
 #ifdef FI_VT_NT
 #define VT_ST(v, p) __builtin_nontemporal_store((v), (p))
 #else
@@ -71,16 +69,12 @@ struct VtArgs {
     float* dval;
     double* part;  // [nblk][3]
     float* sink;   // 2048 floats of scratch for masked-off stores
+    int* bad;      // count of actions outside [0, A) (those rows use a clamped action)
     fi_vtrace_hparams hp;
 };
 
-#ifdef FI_VT_STAMPS
-constexpr size_t kSinkFloats = 2048 + 2 * 20 * 1024;  // + stamps of up to 1024 workgroups
-#else
 constexpr size_t kSinkFloats = 2048;
-#endif
 
-#ifndef FI_VT_SHFLSUM
 // wave-wide double sum in VALU cross-lane moves (no ds_bpermute round trips in the
 // workgroup's tail): rotations 8, 4, 2, 1 inside each 16-lane row by DPP, then the row pairs
 // and halves by gfx950's v_permlane16_swap / v_permlane32_swap. The summation order is
@@ -120,9 +114,6 @@ __device__ __forceinline__ double vt_wave_sum(double v) {
     v += vt_xor_d<32>(v, lane);
     return v;
 }
-#else
-__device__ __forceinline__ double vt_wave_sum(double v) { return wave_sum(v); }
-#endif
 
 __device__ __forceinline__ void block_reduce3(double pg, double base, double ent, double* red,
                                               double* out) {
@@ -162,6 +153,7 @@ __global__ __launch_bounds__(256) void vtrace_column_kernel(VtArgs a) {
             const float* zp = a.pi + e * A;
             const float* zm = a.mu + e * A;
             int at = a.act[e];
+            if ((unsigned)at >= (unsigned)A) atomicAdd(a.bad, 1);
             at = at < 0 ? 0 : (at >= A ? A - 1 : at);
             float mx = -INFINITY, mm = -INFINITY;
             for (int i = 0; i < A; ++i) { mx = fmaxf(mx, zp[i]); mm = fmaxf(mm, zm[i]); }
@@ -225,15 +217,9 @@ struct VtLayout {
     static constexpr int LOGB = TC * ROWB;             // bytes per logits tile (= 256*NW*A)
     static constexpr int SCB = TC * NB * 4;            // bytes per scalar tile (= 256*NW)
     static constexpr int PT = LOGB / 1024;             // 1-KiB pieces per logits tile
-#ifdef FI_VT_MUREG  // mu rows go straight to registers (one chunk ahead): half the LDS per wave
-    static constexpr int MUB = 0;                      // no mu tile
-    static constexpr int TOTB = NW * 16 * 4;           // per-slot wave totals (d, g per column)
-    static constexpr int GLOG = (PT + NW - 1) / NW;    // pi pieces per wave per chunk (j < PT)
-#else
     static constexpr int MUB = LOGB;
     static constexpr int TOTB = 0;
     static constexpr int GLOG = 2 * PT / NW;           // logits pieces per wave per chunk
-#endif
     static constexpr int SCO = LOGB + MUB;             // scalar tiles' offset in a slot
     static constexpr int SLOT = SCO + 4 * SCB + TOTB;  // pi | mu | act | rew | disc | val [| tot]
     static constexpr int RING = 2;
@@ -267,9 +253,6 @@ __device__ __forceinline__ int vt_issue_chunk(const VtArgs& a, const VtRsrc& rs,
 #pragma unroll
     for (int i = I0; i < (I1 < L::GLOG ? I1 : L::GLOG); ++i) {
         const int j = w + L::NW * i;  // wave-uniform piece index: pi (0..PT-1), mu (PT..2PT-1)
-#ifdef FI_VT_MUREG
-        if (j >= L::PT) continue;     // pi pieces only
-#endif
         const int jj = j < L::PT ? j : j - L::PT;
         const int last_row = (jj * 1024 + 1023) / L::ROWB;
         if (last_row < first_row) continue;
@@ -303,7 +286,6 @@ __device__ __forceinline__ int vt_issue_chunk(const VtArgs& a, const VtRsrc& rs,
     return n;
 }
 
-#ifndef FI_VT_SHFLSCAN
 // v from lane ^ S, in VALU cross-lane ops (no LDS round trip): S = 8 by DPP row_ror:8 inside
 // each 16-lane row, S = 16 / 32 by gfx950's v_permlane16_swap / v_permlane32_swap
 template <int S>
@@ -328,7 +310,6 @@ __device__ __forceinline__ void vt_xscan_step(float& sd, float& sg, float& ed, f
     sd = later ? sd + sg * pd : pd + pg * sd;
     sg = sg * pg;
 }
-#endif
 
 template <int A>
 __global__ __launch_bounds__(64 * VtLayout<A>::NW, VtLayout<A>::WPS) void vtrace_lds_kernel(VtArgs a) {
@@ -354,27 +335,9 @@ __global__ __launch_bounds__(64 * VtLayout<A>::NW, VtLayout<A>::WPS) void vtrace
     int issued = vt_issue_chunk<A, 0, NP>(a, rs, lds0, 0, T - L::TC, b0, w, lane);
     int mark = issued;  // VMEM ops issued once the chunk being waited for was queued
     const fi_vtrace_hparams hp = a.hp;
-#ifdef FI_VT_MUREG
-    // this lane's mu row of the next chunk, loaded one chunk ahead. Not counted in `issued`:
-    // they are issued before the chunk's last DMA group (the `mark` point), so they are older
-    // than every op the counted waits let stay in flight, and the B1 wait covers them
-    f32x2 mun[A / 2], mur[A / 2];
-    {
-        const f32x2* src = (const f32x2*)(a.mu + ((size_t)max(T - L::TC + tl, 0) * B + b) * A);
-#pragma unroll
-        for (int i = 0; i < A / 2; ++i) mun[i] = src[i];
-    }
-#endif
 
     float pg = 0.f, base = 0.f, ent = 0.f;
-#ifdef FI_VT_STAMPS  // timing experiment: s_memrealtime stamps of wave 0, written over vs
-    unsigned long long stamp[20];
-    int ns = 0;
-    stamp[ns++] = __builtin_amdgcn_s_memrealtime();
-#define VT_STAMP() if (ns < 20) stamp[ns++] = __builtin_amdgcn_s_memrealtime()
-#else
 #define VT_STAMP()
-#endif
     for (int k = 0; k < nchunks; ++k) {
         const int slot = k & 1;
         const int t0 = T - L::TC * (k + 1);
@@ -382,23 +345,11 @@ __global__ __launch_bounds__(64 * VtLayout<A>::NW, VtLayout<A>::WPS) void vtrace
         lds_barrier();  // B1: chunk k landed for every wave; slot (k+1)&1 fully consumed
         VT_STAMP();
         const bool more = k + 1 < nchunks;
-#ifdef FI_VT_MUREG
-#pragma unroll
-        for (int i = 0; i < A / 2; ++i) mur[i] = mun[i];
-        if (more) {
-            const f32x2* src = (const f32x2*)(a.mu + ((size_t)max(t0 - L::TC + tl, 0) * B + b) * A);
-#pragma unroll
-            for (int i = 0; i < A / 2; ++i) mun[i] = src[i];
-        }
-#endif
         if (more) issued += vt_issue_chunk<A, 0, G1>(a, rs, lds0, slot ^ 1, t0 - L::TC, b0, w, lane);
         VT_STAMP();
-#ifndef FI_VT_DMAONLY
         char* sl = smem + slot * L::SLOT;
         float* zpi = (float*)sl + tl * L::ROWF + c * A;
-#ifndef FI_VT_MUREG
         float* zmu = (float*)(sl + L::LOGB) + tl * L::ROWF + c * A;
-#endif
         const int* sact = (const int*)(sl + L::SCO);
         const float* srew = (const float*)(sl + L::SCO + L::SCB);
         const float* sdisc = (const float*)(sl + L::SCO + 2 * L::SCB);
@@ -413,35 +364,12 @@ __global__ __launch_bounds__(64 * VtLayout<A>::NW, VtLayout<A>::WPS) void vtrace
 #pragma unroll
         for (int i = 0; i < A / 2; ++i) {
             zp2[i] = *(const f32x2*)(zpi + 2 * i);
-#ifdef FI_VT_MUREG
-            zm2[i] = mur[i];
-#else
             zm2[i] = *(const f32x2*)(zmu + 2 * i);
-#endif
         }
         int at = sact[tl * L::NB + c];
+        if (valid && (unsigned)at >= (unsigned)A) atomicAdd(a.bad, 1);
         at = at < 0 ? 0 : (at >= A ? A - 1 : at);
-#ifdef FI_VT_MUREG
-        float zma = zm2[0].x;
-#pragma unroll
-        for (int i = 0; i < A / 2; ++i) {
-            zma = at == 2 * i ? zm2[i].x : zma;
-            zma = at == 2 * i + 1 ? zm2[i].y : zma;
-        }
-        const float zpa = zpi[at];
-#elif !defined(FI_VT_REGAT)
         const float zpa = zpi[at], zma = zmu[at];
-#else
-        // the taken action's logits picked from the registers (no second, dependent LDS read)
-        float zpa = zp2[0].x, zma = zm2[0].x;
-#pragma unroll
-        for (int i = 0; i < A / 2; ++i) {
-            zpa = at == 2 * i ? zp2[i].x : zpa;
-            zpa = at == 2 * i + 1 ? zp2[i].y : zpa;
-            zma = at == 2 * i ? zm2[i].x : zma;
-            zma = at == 2 * i + 1 ? zm2[i].y : zma;
-        }
-#endif
         const float rw = srew[tl * L::NB + c];
         const float g = sdisc[tl * L::NB + c];
         const float v = sval[tl * L::NB + c];
@@ -479,7 +407,6 @@ __global__ __launch_bounds__(64 * VtLayout<A>::NW, VtLayout<A>::WPS) void vtrace
         float d = valid ? rho * (rw + g * vn - v) : 0.f;
         float gg = valid ? g * cc : 1.f;
 
-#ifndef FI_VT_SHFLSCAN
         // butterfly over the wave's 8 rows (lane ^ 8, ^ 16, ^ 32): (sd, sg) = the composition
         // of the lane's current row segment, (ed, eg) = the composition of the rows after this
         // one inside it; at the end (sd, sg) is the wave total in every row
@@ -488,22 +415,10 @@ __global__ __launch_bounds__(64 * VtLayout<A>::NW, VtLayout<A>::WPS) void vtrace
         vt_xscan_step<8>(d, gg, ed, eg, lane);
         vt_xscan_step<16>(d, gg, ed, eg, lane);
         vt_xscan_step<32>(d, gg, ed, eg, lane);
-#else
-        // inclusive suffix composition over the wave's 8 rows (lanes +8, +16, +32)
-#pragma unroll
-        for (int s = 8; s < 64; s <<= 1) {
-            const float d2 = __shfl_down(d, s, 64), g2 = __shfl_down(gg, s, 64);
-            if (lane + s < 64) { d = d + gg * d2; gg = gg * g2; }
-        }
-#endif
         if (more) issued += vt_issue_chunk<A, G2, NP>(a, rs, lds0, slot ^ 1, t0 - L::TC, b0, w, lane);
         mark = issued;  // the wait for chunk k+1 ignores the stores issued after this point
         // wave total -> this wave's own first mu row (no other wave reads it)
-#ifdef FI_VT_MUREG
-        float* tot = (float*)(sl + L::SCO + 4 * L::SCB) + 16 * w;
-#else
         float* tot = (float*)(sl + L::LOGB) + (8 * w) * L::ROWF;
-#endif
         if (lane < 8) {
             tot[c] = d;
             tot[8 + c] = gg;
@@ -515,23 +430,13 @@ __global__ __launch_bounds__(64 * VtLayout<A>::NW, VtLayout<A>::WPS) void vtrace
         float carry_new = carry;
 #pragma unroll
         for (int w2 = L::NW - 1; w2 >= 0; --w2) {
-#ifdef FI_VT_MUREG
-            const float* t2 = (const float*)(sl + L::SCO + 4 * L::SCB) + 16 * w2;
-#else
             const float* t2 = (const float*)(sl + L::LOGB) + (8 * w2) * L::ROWF;
-#endif
             carry_new = t2[c] + t2[8 + c] * carry_new;
             if (w2 == w + 1) acc_in = carry_new;
         }
         if (w == L::NW - 1) acc_in = carry;
-#ifndef FI_VT_SHFLSCAN
         const float acc_nx = ed + eg * acc_in;
         const float acc = d_own + g_own * acc_nx;
-#else
-        const float acc = d + gg * acc_in;
-        const float acc_up = __shfl_down(acc, 8, 64);
-        const float acc_nx = (r == 7) ? acc_in : acc_up;
-#endif
         const float vs_t = v + acc;
         const float vs_n = vn + acc_nx;
         const float adv = pgr * (rw + g * vs_n - v);
@@ -546,24 +451,14 @@ __global__ __launch_bounds__(64 * VtLayout<A>::NW, VtLayout<A>::WPS) void vtrace
             const float al = inv * (adv - ec * (plogp + lse)), be = inv * ec;
             const f32x2 al2 = {al, al};
 #pragma unroll
-#ifndef FI_VT_REGAT
             for (int i = 0; i < A / 2; ++i) *(f32x2*)(zpi + 2 * i) = e2[i] * (zp2[i] * be + al2);
             zpi[at] -= adv;
-#else
-            for (int i = 0; i < A / 2; ++i) {  // - adv at the taken action, in registers
-                f32x2 dz = e2[i] * (zp2[i] * be + al2);
-                dz.x = at == 2 * i ? dz.x - adv : dz.x;
-                dz.y = at == 2 * i + 1 ? dz.y - adv : dz.y;
-                *(f32x2*)(zpi + 2 * i) = dz;
-            }
-#endif
         }
         if (valid) {
             pg += -adv * lpa;
             base += 0.5f * acc * acc;
             ent += plogp;
         }
-#ifndef FI_VT_NOSTORE
         // Stores. Every chunk but the last (the only one holding t < 0) stores with the full
         // wave, so the per-wave VMEM count used by the next chunk's wait is exact; the last
         // chunk masks freely (nothing waits on its count). Rows: vs/pg_adv/dvalue 32 B per
@@ -599,20 +494,11 @@ __global__ __launch_bounds__(64 * VtLayout<A>::NW, VtLayout<A>::WPS) void vtrace
                 issued += (REM2 + 63) / 64;
             }
         }
-#endif
-#endif  // FI_VT_DMAONLY
         VT_STAMP();
     }
-#ifdef FI_VT_TAILWAIT
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
     // no vmcnt(0) here: the last chunk issues no LDS-DMA (only global stores are in flight),
     // so the loss-partial reduction below can overlap the store drain
     VT_STAMP();
-#ifdef FI_VT_STAMPS
-    if (tid == 0)
-        for (int i = 0; i < 20; ++i) ((unsigned long long*)(a.sink + 2048))[blockIdx.x * 20 + i] = i < ns ? stamp[i] : 0ull;
-#endif
     __syncthreads();
     // per-workgroup loss partials; summed in a fixed order by vtrace_finalize_kernel or, in
     // the learner step, by the gradient-norm kernel that runs anyway (no extra launch, no
@@ -621,7 +507,8 @@ __global__ __launch_bounds__(64 * VtLayout<A>::NW, VtLayout<A>::WPS) void vtrace
 }
 
 __global__ __launch_bounds__(256) void vtrace_finalize_kernel(const double* __restrict__ part,
-                                                              int nblk, double* losses) {
+                                                              int nblk, double* losses,
+                                                              const int* bad) {
     __shared__ double red[4 * 3];
     double s0 = 0, s1 = 0, s2 = 0;
     for (int i = threadIdx.x; i < nblk; i += 256) {
@@ -630,6 +517,9 @@ __global__ __launch_bounds__(256) void vtrace_finalize_kernel(const double* __re
         s2 += part[(size_t)i * 3 + 2];
     }
     block_reduce3(s0, s1, s2, red, losses);
+    // an action outside [0, A) anywhere in the batch poisons the loss scalars (the oracle
+    // rejects such a batch; the standalone entry point has no synchronous status to return)
+    if (threadIdx.x < 3 && bad && *bad != 0) losses[threadIdx.x] = __builtin_nan("");
 }
 
 // ------------------------------------------------------------------------------------
@@ -637,10 +527,15 @@ __global__ __launch_bounds__(256) void vtrace_finalize_kernel(const double* __re
 // ------------------------------------------------------------------------------------
 static size_t vt_nblk_max(int B) { return (size_t)std::max((B + 7) / 8, (B + 255) / 256); }
 
+// workspace: [sink floats][loss partials, 256-B padded][int bad-action counter, 256 B]
+static size_t vt_part_bytes(int B) { return (vt_nblk_max(B) * 3 * sizeof(double) + 255) & ~(size_t)255; }
 size_t vtrace_workspace_bytes(int T, int B, int A) {
     (void)T;
     (void)A;
-    return kSinkFloats * sizeof(float) + ((vt_nblk_max(B) * 3 * sizeof(double) + 255) & ~(size_t)255);
+    return kSinkFloats * sizeof(float) + vt_part_bytes(B) + 256;
+}
+static int* vt_bad_counter(void* ws, int B) {
+    return (int*)((char*)ws + kSinkFloats * sizeof(float) + vt_part_bytes(B));
 }
 
 template <int A>
@@ -654,7 +549,7 @@ int vtrace_launch(int variant, int T, int B, int A, const float* pi, const float
                   const int32_t* act, const float* rew, const float* disc, const float* val,
                   const fi_vtrace_hparams& hp, float* vs, float* adv, float* dlog, float* dval,
                   double* losses, void* ws, size_t ws_bytes, hipStream_t stream, bool finalize,
-                  int* nblk_out) {
+                  int* nblk_out, int* bad) {
     FI_REQUIRE(T >= 1 && B >= 1 && A >= 1 && A <= 64, "vtrace: bad shape");
     FI_REQUIRE(pi && mu && act && rew && disc && val && dlog && dval && ws, "vtrace: null pointer");
     finalize = finalize && losses;  // losses == NULL: partials stay in the workspace
@@ -666,8 +561,17 @@ int vtrace_launch(int variant, int T, int B, int A, const float* pi, const float
     a.sink = (float*)ws;
     a.part = (double*)((char*)ws + kSinkFloats * sizeof(float));
     a.hp = hp;
-    bool use_lds = variant == 1 || (variant == 0 && lds_supported(A, B));
+    a.bad = bad;
+    if (!bad) {  // standalone call: count into the workspace, finalize turns it into NaN losses
+        a.bad = vt_bad_counter(ws, B);
+        FI_HIP_CHECK(hipMemsetAsync(a.bad, 0, sizeof(int), stream));
+    }
+    // the LDS kernel's buffer descriptors and DMA offsets are 32-bit: T*B*A*4 must stay
+    // below 2^31 bytes (else the column kernel, 64-bit indexing, runs)
+    const bool fits32 = (size_t)T * B * A * sizeof(float) < ((size_t)1 << 31);
+    bool use_lds = variant == 1 || (variant == 0 && lds_supported(A, B) && fits32);
     FI_REQUIRE(!(variant == 1 && !lds_supported(A, B)), "vtrace: LDS kernel needs B%8==0, even A<=20");
+    FI_REQUIRE(!(variant == 1 && !fits32), "vtrace: LDS kernel needs T*B*A*4 < 2^31 bytes");
     int nblk;
     if (use_lds) {
         FI_REQUIRE(vs && adv, "vtrace: LDS kernel writes vs and pg_adv (non-null)");
@@ -694,7 +598,7 @@ int vtrace_launch(int variant, int T, int B, int A, const float* pi, const float
     }
     FI_HIP_CHECK(hipGetLastError());
     if (nblk_out) *nblk_out = nblk;
-    if (finalize) return vtrace_finalize_launch(ws, nblk, losses, stream);
+    if (finalize) return vtrace_finalize_launch(ws, nblk, losses, stream, a.bad);
     return FI_OK;
 }
 
@@ -702,9 +606,9 @@ const double* vtrace_partials(const void* ws) {
     return (const double*)((const char*)ws + kSinkFloats * sizeof(float));
 }
 
-int vtrace_finalize_launch(void* ws, int nblk, double* losses, hipStream_t stream) {
+int vtrace_finalize_launch(void* ws, int nblk, double* losses, hipStream_t stream, const int* bad) {
     const double* part = (const double*)((char*)ws + kSinkFloats * sizeof(float));
-    hipLaunchKernelGGL(vtrace_finalize_kernel, dim3(1), dim3(256), 0, stream, part, nblk, losses);
+    hipLaunchKernelGGL(vtrace_finalize_kernel, dim3(1), dim3(256), 0, stream, part, nblk, losses, bad);
     FI_HIP_CHECK(hipGetLastError());
     return FI_OK;
 }

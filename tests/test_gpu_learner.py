@@ -285,3 +285,38 @@ def test_state_checkpoint_resume_is_bit_exact():
     from freeimpala_amd._abi import FiError
     with pytest.raises(FiError):
         L2.load_state(blob[:-4])
+
+
+def test_out_of_range_action_rejects_batch(orc):
+    """A record whose action lies outside [0, A) (corrupt entry, or actors run with another
+    --num-actions) is not clamped into a plausible gradient: the step returns FI_ERR_INVALID,
+    the parameters, Adam moments and version stay as they were, and the next valid batch
+    steps normally (the oracle rejects the same batch with -3). Sync, async and staged forms."""
+    from freeimpala_amd._abi import FiError
+    from freeimpala_amd.learner import pack_records
+    T, B = 4, 32
+    good = orc.synth_batch(41, T=T, B=B, A=18, D=128)
+    bad = {k: v.copy() for k, v in good.items()}
+    bad["actions"][2, 5] = 18
+    bad["actions"][0, 0] = -1
+    with pytest.raises(Exception):
+        orc.vtrace_loss(np.zeros((T, B, 18), np.float32), bad["mu"], bad["actions"], bad["rewards"],
+                        bad["discounts"], np.zeros((T + 1, B), np.float32))
+    pk = lambda b: pack_records(b["obs"], b["mu"], b["actions"], b["rewards"], b["discounts"],
+                                entry_size=T + 1)
+    L, R = mk(T=T, B=B, seed=6, optimizer="adam"), mk(T=T, B=B, seed=6, optimizer="adam")
+    R.step(pk(good))
+    L.step(pk(good))
+    p1, m1 = L.get_params(), L.tensor("adam_m")
+    with pytest.raises(FiError, match="outside"):
+        L.step(pk(bad))
+    np.testing.assert_array_equal(L.get_params(), p1)
+    np.testing.assert_array_equal(L.tensor("adam_m"), m1)
+    L.step_async(pk(bad))
+    with pytest.raises(FiError, match="outside"):
+        L.wait()
+    np.testing.assert_array_equal(L.get_params(), p1)
+    s = L.step(pk(good))
+    r = R.step(pk(good))
+    assert s["version"] == r["version"] == 2
+    np.testing.assert_array_equal(L.get_params(), R.get_params())

@@ -125,3 +125,16 @@ def test_vtrace_variants_agree_bitwise_on_losses_order_free_fields(orc):
     b = run_vtrace(*case, variant=2)
     compare(a, b)
     assert np.all(a["dvalue"][-1] == 0) and np.all(b["dvalue"][-1] == 0)
+
+
+@pytest.mark.parametrize("variant", [1, 2])
+def test_vtrace_out_of_range_action_poisons_losses(variant):
+    """Standalone kernels: an action outside [0, A) makes the finalised loss scalars NaN
+    (the device-side signal of a rejected batch) instead of a silently clamped result."""
+    pi, mu, act, rew, disc, val = rand_case(5, 8, 16, 6)
+    act[3, 7] = 6
+    out = run_vtrace(pi, mu, act, rew, disc, val, variant=variant)
+    assert np.isnan(out["losses"]).all()
+    act[3, 7] = 2
+    out = run_vtrace(pi, mu, act, rew, disc, val, variant=variant)
+    assert np.isfinite(out["losses"]).all()
