@@ -108,6 +108,10 @@ def download_ptr(ptr: int, dtype, shape) -> np.ndarray:
     return out
 
 
+def copy_d2d(dst: int, src: int, nbytes: int) -> None:
+    _chk(hip().hipMemcpy(dst, src, nbytes, D2D), "hipMemcpy D2D")
+
+
 def upload_ptr(ptr: int, a: np.ndarray) -> None:
     a = np.ascontiguousarray(a)
     _chk(hip().hipMemcpy(ptr, a.ctypes.data, a.nbytes, H2D), "hipMemcpy H2D")

@@ -165,36 +165,54 @@ class DeviceLearner:
         self.sync()
         hip.upload_ptr(p, a)
 
-    def replay_vtrace(self, n: int = 20) -> float:
+    def replay_vtrace(self, n: int = 20, sets: int = 1) -> float:
         """Mean device ms of the fused V-trace kernel alone: n back-to-back launches of
-        fi_vtrace_loss_fp32 (no loss finalisation) on this learner's resident tensors,
-        HIP events around the burst. Inputs are read-only and the outputs are rewritten with
-        identical values, so the learner state is unchanged."""
+        fi_vtrace_loss_fp32 (no loss finalisation), HIP events around the burst.
+
+        sets = 1: every launch reads this learner's resident tensors (~100 MB at T=100,
+        B=4096), which stay in the 256 MB Infinity Cache between launches -- a WARM figure.
+        sets = k > 1: launches rotate over k disjoint copies of the inputs and outputs
+        (k x ~100 MB, > 256 MB for k >= 3), so each launch finds its tensors evicted by the
+        k-1 launches before it -- the COLD (HBM) figure. Inputs are read-only and the
+        learner's own outputs are rewritten with identical values: its state is unchanged."""
         T, B, A = self.T, self.B, self.A
-        ptr = {k: self.tensor_ptr(k)[0] for k in ("logits", "mu", "actions", "rewards", "discounts",
-                                                   "values", "vs", "pg_adv", "dlogits", "dvalue")}
+        names = ("logits", "mu", "actions", "rewards", "discounts", "values", "vs", "pg_adv",
+                 "dlogits", "dvalue")
+        base = {k: self.tensor_ptr(k) for k in names}
         hp = self.cfg.hp
         wsb = lib().fi_vtrace_workspace_bytes(T, B, A)
-        ws = hip.DeviceBuffer(wsb)
         stream = self.stream
+        self.sync()
+        owned = []
+        sets_ptr = [{k: v[0] for k, v in base.items()}]
+        for _ in range(1, max(1, sets)):
+            d = {}
+            for k, (ptr, nb) in base.items():
+                buf = hip.DeviceBuffer(nb)
+                hip.copy_d2d(buf.ptr, ptr, nb)
+                owned.append(buf)
+                d[k] = buf.ptr
+            sets_ptr.append(d)
+        ws = [hip.DeviceBuffer(wsb) for _ in sets_ptr]
 
-        def launch():
+        def launch(i):
+            ptr, w = sets_ptr[i % len(sets_ptr)], ws[i % len(sets_ptr)]
             check(lib().fi_vtrace_loss_fp32(
                 T, B, A, ptr["logits"], ptr["mu"], ptr["actions"], ptr["rewards"], ptr["discounts"],
                 ptr["values"], C.byref(hp), ptr["vs"], ptr["pg_adv"], ptr["dlogits"], ptr["dvalue"],
-                None, ws.ptr, wsb, stream), "fi_vtrace_loss_fp32")
+                None, w.ptr, wsb, stream), "fi_vtrace_loss_fp32")
 
-        self.sync()
-        for _ in range(3):
-            launch()
+        for i in range(max(3, len(sets_ptr))):
+            launch(i)
         e0, e1 = hip.Event(), hip.Event()
         e0.record(stream)
-        for _ in range(n):
-            launch()
+        for i in range(n):
+            launch(i)
         e1.record(stream)
         self.sync()
         ms = e0.elapsed_ms(e1) / n
-        ws.free()
+        for b in owned + ws:
+            b.free()
         return ms
 
     # --- data parallel
