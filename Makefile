@@ -11,7 +11,7 @@ SRCS := $(CSRC)/vtrace.hip $(CSRC)/gemm_f32.hip $(CSRC)/misc.hip $(CSRC)/atari.h
 OBJS := $(patsubst $(CSRC)/%,$(OBJDIR)/%.o,$(SRCS))
 HDRS := $(wildcard $(CSRC)/*.h) include/fi_learner.h
 
-all: $(LIBDIR)/libfi_learner.so oracle host
+all: $(LIBDIR)/libfi_learner.so oracle host tools
 
 $(OBJDIR)/%.hip.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
@@ -29,11 +29,20 @@ oracle:
 	$(MAKE) -s -C oracle
 
 # C++ host-side check program (include/freeimpala_amd/device_learner.hpp over the C ABI)
-host: build/host_learner_check
+host: build/host_learner_check build/replay_check
+build/replay_check: tests/cpp/replay_check.cpp $(wildcard include/freeimpala_amd/*.hpp) include/fi_learner.h $(LIBDIR)/libfi_learner.so
+	@mkdir -p build
+	g++ -std=c++17 -O2 -Wall -Wextra -Iinclude $< -o $@ -L$(LIBDIR) -lfi_learner -pthread '-Wl,-rpath,$$ORIGIN/../$(LIBDIR)' -Wl,-rpath,/opt/rocm/lib
 build/host_learner_check: tests/cpp/host_learner_check.cpp include/freeimpala_amd/device_learner.hpp include/fi_learner.h $(LIBDIR)/libfi_learner.so
 	@mkdir -p build
 	g++ -std=c++17 -O2 -Wall -Iinclude $< -o $@ -L$(LIBDIR) -lfi_learner -pthread '-Wl,-rpath,$$ORIGIN/../$(LIBDIR)' -Wl,-rpath,/opt/rocm/lib
 
+# the cmd/freeimpala-shaped binary on freeimpala_amd::Learner (include/freeimpala_amd/learner.hpp)
+tools: build/fi_freeimpala
+build/fi_freeimpala: tools/fi_freeimpala.cpp $(wildcard include/freeimpala_amd/*.hpp) include/fi_learner.h $(LIBDIR)/libfi_learner.so
+	@mkdir -p build
+	g++ -std=c++17 -O2 -Wall -Wextra -Iinclude $< -o $@ -L$(LIBDIR) -lfi_learner -pthread '-Wl,-rpath,$$ORIGIN/../$(LIBDIR)' -Wl,-rpath,/opt/rocm/lib
+
 clean:
 	rm -rf build $(LIBDIR)
-.PHONY: all oracle host clean
+.PHONY: all oracle host tools clean

@@ -109,6 +109,44 @@ struct LearnerConfig {
         return c;
     }
 
+    // Learner flags through a strict parser (freeimpala_amd::ArgumentParser or the argparse
+    // library of the reference binaries): the reference's own -p/--players, -M/--batch-size and
+    // -S/--entry-size (registered by its setupArgumentParser, cmd/freeimpala/main.cpp:45-72)
+    // plus the flags add_learner_arguments() registers. Throws std::invalid_argument.
+    template <class Parser>
+    static LearnerConfig from_parser(const Parser& program, LearnerConfig c = LearnerConfig()) {
+        auto num = [](const std::string& f, const std::string& v) -> double {
+            char* end = nullptr;
+            const double x = std::strtod(v.c_str(), &end);
+            if (v.empty() || (end && *end)) throw std::invalid_argument("bad value for " + f + ": " + v);
+            return x;
+        };
+        auto str = [&](const char* f) { return program.template get<std::string>(f); };
+        c.players = (size_t)program.template get<int>("--players");
+        c.batch_size = (size_t)program.template get<int>("--batch-size");
+        c.entry_size = (size_t)program.template get<int>("--entry-size");
+        c.seq_length = (size_t)num("--seq-length", str("--seq-length"));
+        c.arch = str("--learner-arch");
+        c.num_actions = (int)num("--num-actions", str("--num-actions"));
+        c.obs_dim = (int)num("--obs-dim", str("--obs-dim"));
+        c.hidden = (int)num("--hidden", str("--hidden"));
+        c.optimizer = str("--optimizer");
+        c.publish = str("--publish");
+        c.lr = (float)num("--lr", str("--lr"));
+        c.max_grad_norm = (float)num("--max-grad-norm", str("--max-grad-norm"));
+        c.gamma = (float)num("--gamma", str("--gamma"));
+        c.seed = (uint64_t)num("--learner-seed", str("--learner-seed"));
+        const char* argv[] = {"", "--devices", nullptr};
+        const std::string dev = str("--devices");
+        argv[2] = dev.c_str();
+        // (validation as from_args; an entry size too small for seq_length + 1 records is left
+        // to the Learner, which lowers seq_length with a warning)
+        LearnerConfig v = c;
+        v.entry_size = 0;
+        c.devices = from_args(3, argv, v).devices;
+        return c;
+    }
+
     // The C-ABI configuration of player p's handle.
     fi_learner_config abi_config(size_t p) const {
         fi_learner_config k;
@@ -130,6 +168,30 @@ struct LearnerConfig {
         return k;
     }
 };
+
+// Registers the device-learner flags with a strict parser (string-valued, so the same calls
+// work on argparse::ArgumentParser); values are checked by LearnerConfig::from_parser. --seed
+// stays the reference's own (rand() seeding, main.cpp:111-114): parameter init is
+// --learner-seed.
+template <class Parser>
+void add_learner_arguments(Parser& program) {
+    const LearnerConfig d;
+    program.add_argument("--seq-length").help("Trajectory length T (entries carry T+1 records)")
+        .default_value(std::to_string(d.seq_length));
+    program.add_argument("--learner-arch").help("Policy network: mlp | atari").default_value(d.arch);
+    program.add_argument("--num-actions").help("Number of actions A").default_value(std::to_string(d.num_actions));
+    program.add_argument("--obs-dim").help("MLP observation width (<= 128)").default_value(std::to_string(d.obs_dim));
+    program.add_argument("--hidden").help("MLP hidden width").default_value(std::to_string(d.hidden));
+    program.add_argument("--optimizer").help("adam | sgd").default_value(d.optimizer);
+    program.add_argument("--publish").help("Published weights dtype: fp32 | bf16").default_value(d.publish);
+    program.add_argument("--lr").help("Learning rate").default_value(std::string("0.0005"));
+    program.add_argument("--max-grad-norm").help("Global-norm gradient clip (<= 0: off)")
+        .default_value(std::string("40"));
+    program.add_argument("--gamma").help("Discount of the synthetic trajectories").default_value(std::string("0.99"));
+    program.add_argument("--learner-seed").help("Parameter-initialisation seed").default_value(std::to_string(d.seed));
+    program.add_argument("--devices").help("HIP devices, comma separated (player p -> devices[p % n])")
+        .default_value(std::string("0"));
+}
 
 class DeviceLearner {
 public:

@@ -19,7 +19,8 @@ EXE = os.path.join(ROOT, "build", "host_learner_check")
 
 def _build():
     src = os.path.join(ROOT, "tests", "cpp", "host_learner_check.cpp")
-    if not os.path.exists(EXE) or os.path.getmtime(EXE) < os.path.getmtime(src):
+    if not os.path.exists(EXE) or (os.path.isdir(os.path.join(ROOT, "build", "obj")) and
+                                   os.path.getmtime(EXE) < os.path.getmtime(src)):
         subprocess.run(["make", "-s", "-C", ROOT, "host"], check=True)
     return EXE
 
