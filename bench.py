@@ -282,6 +282,8 @@ def main():
         "kernel_ms_per_step": {k: round(v, 4) for k, v in sorted(per_step.items(), key=lambda x: -x[1])},
         "phase_ms": {k: round(v, 4) for k, v in phases.items() if k != "steps"},
         "final_loss": st["total_loss"], "grad_norm": st["grad_norm"],
+        # RCCL's own view of the data-parallel communicator (ncclCommCount / ncclCommUserRank)
+        "comm": L.comm_info(),
     }
     if rank == 0 and N == 1 and not args.no_cpu_baseline:
         # every core this process may use: the box's OMP_NUM_THREADS share when set (16 per GPU

@@ -74,6 +74,8 @@ SIGNATURES = {
     "fi_comm_unique_id_bytes": ([], C.c_int),
     "fi_comm_get_unique_id": ([_P, C.c_size_t], C.c_int),
     "fi_learner_attach_comm": ([_P, _P, C.c_size_t, C.c_int, C.c_int], C.c_int),
+    "fi_comm_init_all": ([_P, C.c_int], C.c_int),
+    "fi_learner_comm_info": ([_P, _P, _P, _P], C.c_int),
     "fi_learner_tensor": ([_P, C.c_char_p, C.POINTER(_P), C.POINTER(C.c_size_t)], C.c_int),
     "fi_learner_set_profiling": ([_P, C.c_int], C.c_int),
     "fi_learner_phase_times": ([_P, C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_int)], C.c_int),

@@ -24,6 +24,14 @@ struct TagScope {
     }
 };
 
+// gradient-ready hook: the backward pass calls ready(off, n) once grads[off, off+n) hold
+// their final values for this step (enqueued on the stream), latest layers first; the
+// learner starts that bucket's all-reduce on its comm stream while the backward continues
+struct GradReadyHook {
+    virtual int ready(size_t off, size_t n) = 0;
+    virtual ~GradReadyHook() {}
+};
+
 struct AtariNet {
     static constexpr size_t kFrameBytes = 84 * 84 * 4;
     int B = 0, T = 0, A = 0, N = 0;  // N = (T+1)*B frames
@@ -38,7 +46,7 @@ int atari_sync_weights(AtariNet* n, const float* params, hipStream_t s);
 int atari_forward(AtariNet* n, const uint8_t* frames, float* logits, float* values, hipStream_t s,
                   KernelTagger* tg = nullptr);
 int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, const float* dvalue,
-                   float* grads, hipStream_t s, KernelTagger* tg = nullptr);
+                   float* grads, hipStream_t s, KernelTagger* tg = nullptr, GradReadyHook* gr = nullptr);
 bool atari_tensor(AtariNet* n, const char* name, void** p, size_t* bytes);
 
 }  // namespace fi

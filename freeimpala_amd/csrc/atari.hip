@@ -883,7 +883,7 @@ int atari_forward(AtariNet* n, const uint8_t* frames, float* logits, float* valu
 }
 
 int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, const float* dvalue,
-                   float* grads, hipStream_t s, KernelTagger* tg) {
+                   float* grads, hipStream_t s, KernelTagger* tg, GradReadyHook* gr) {
     AtariImpl* I = impl(n);
     const int N = I->N, A = I->A, O = A + 1;
     const Offsets& o = I->off;
@@ -914,6 +914,9 @@ int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, con
     // fc (hipBLASLt): wgrad straight into the gradient blob, bias = column sums of dh,
     // dgrad -> da3 unmasked (conv3's backward applies the a3 ReLU mask as it loads da3)
     FI_A("fc_wgrad", fc_blaslt_wgrad(I->fc, I->a3, I->dh, grads + o.fcw, s));
+    // buckets in reverse layer order: fc + heads (95 % of the gradient bytes) reduce while
+    // fc dgrad, conv3 and conv2/conv1 backward run
+    if (gr && (rc = gr->ready(o.fcw, o.total - o.fcw))) return rc;
     FI_A("fc_dgrad", fc_blaslt_dgrad(I->fc, I->dh, I->wb.fcB, I->da3, s));
     // conv3: wgrad [576][64] + bias, dgrad -> da2 (masked by a2)
     if (I->fr) {
@@ -921,6 +924,7 @@ int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, con
         FI_A("conv3_bwd", conv3_bwd_fr_launch(I->a2, I->da3, I->a3, I->wb.c3D, I->da2, slab, cs, N, grid, s));
         FI_A("reduce_slabs", reduce_slabs(slab, grid, (size_t)C3K * C3O, grads + o.c3w, s));
         FI_A("reduce_slabs", reduce_slabs(cs, grid, (size_t)C3O, grads + o.c3b, s));
+        if (gr && (rc = gr->ready(o.c3w, o.fcw - o.c3w))) return rc;
     } else {
         FI_A("relu_mask", relu_mask_bf16(I->da3, I->a3, (size_t)N * FCK, s));
         FI_A("conv3_wgrad", (wgrad<128, 64, 2, 2>(ConvGather<9, 64, 3, 1, 7>{I->a2, N * P3}, RowsBf16{I->da3, N * P3, C3O},
@@ -930,6 +934,7 @@ int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, con
         FI_A("conv3_dgrad", (gemm<128, 64, 2, 2>(DgradGather<9, 3, 1, 7, 64>{I->da3, N, I->cs3},
                                   ClassRows{I->wb.c3D, 64, C3K, I->cs3, (size_t)64 * C3K, nullptr},
                                   EpiDgrad<9, 1>{I->da2, I->a2, N, I->cs3, 64}, I->cs3, 64, C3K, s)));
+        if (gr && (rc = gr->ready(o.c3w, o.fcw - o.c3w))) return rc;
     }
     // conv2 backward + conv1 wgrad fused: da1 stays in LDS (written to HBM only with FI_KEEP_DA1)
     if (I->fr && I->fuse21) {
@@ -942,6 +947,7 @@ int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, con
         FI_A("reduce_slabs", reduce_slabs(cs, grid, (size_t)C2O, grads + o.c2b, s));
         FI_A("reduce_slabs", reduce_slabs(slab1, grid, (size_t)C1K * C1O, grads + o.c1w, s));
         FI_A("reduce_slabs", reduce_slabs(cs1, 4 * grid, (size_t)C1O, grads + o.c1b, s));
+        if (gr && (rc = gr->ready(0, o.c3w))) return rc;
         return FI_OK;
     }
     // conv2: wgrad [512][64] + bias, dgrad -> da1 (4 parity classes, masked by a1)
@@ -971,6 +977,7 @@ int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, con
         FI_A("reduce_slabs", reduce_slabs(slab, SPL_C1, (size_t)C1K * C1O, grads + o.c1w, s));
         FI_A("reduce_slabs", reduce_slabs(cs, SPL_C1, (size_t)C1O, grads + o.c1b, s));
     }
+    if (gr && (rc = gr->ready(0, o.c3w))) return rc;
 #undef FI_A
     return FI_OK;
 }

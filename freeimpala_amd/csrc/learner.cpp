@@ -96,6 +96,12 @@ struct fi_learner {
     // data parallel
     ncclComm_t comm = nullptr;
     int rank = 0, nranks = 1;
+    // bucketed gradient all-reduce: buckets start on comm_stream as the backward finalises
+    // them (reverse layer order); the optimizer waits for the last one (comm_done)
+    hipStream_t comm_stream = nullptr;
+    std::vector<hipEvent_t> bucket_ev;
+    hipEvent_t comm_done = nullptr;
+    int buckets = 0;  // buckets issued in the last step (introspection)
     // bookkeeping
     uint64_t version = 0;
     int step_count = 0;
@@ -197,6 +203,9 @@ static void destroy(fi_learner* l) {
     if (l->stream) hipStreamSynchronize(l->stream);
     if (l->copy_stream) hipStreamSynchronize(l->copy_stream);
     if (l->comm) ncclCommDestroy(l->comm);
+    for (hipEvent_t e : l->bucket_ev) hipEventDestroy(e);
+    if (l->comm_done) hipEventDestroy(l->comm_done);
+    if (l->comm_stream) hipStreamDestroy(l->comm_stream);
     atari_destroy(l->atari);
     for (void* p : l->allocs) hipFree(p);
     for (int i = 0; i < 2; ++i) {
@@ -404,6 +413,40 @@ static void collect_tags(fi_learner* l) {
     l->tag_used = 0;
 }
 
+// Gradient buckets in reverse layer order: once the backward has enqueued
+// the final write of grads[off, off+n), an event on the compute stream gates that bucket's
+// in-place ncclAllReduce(sum) on comm_stream, so the reduction of the fc/heads gradients
+// (95 % of the Atari net's bytes) overlaps the conv backward. Every rank issues the same
+// buckets in the same order. Without a communicator the hook does nothing.
+struct BucketAllReduce : GradReadyHook {
+    fi_learner* l;
+    int n = 0;
+    explicit BucketAllReduce(fi_learner* l_) : l(l_) {}
+    int ready(size_t off, size_t count) override {
+        if (!l->comm || count == 0) return FI_OK;
+        if ((size_t)n >= l->bucket_ev.size()) {
+            hipEvent_t e;
+            FI_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            l->bucket_ev.push_back(e);
+        }
+        FI_HIP_CHECK(hipEventRecord(l->bucket_ev[n], l->stream));
+        FI_HIP_CHECK(hipStreamWaitEvent(l->comm_stream, l->bucket_ev[n], 0));
+        ++n;
+        ncclResult_t r = ncclAllReduce(l->grads + off, l->grads + off, count, ncclFloat, ncclSum,
+                                       l->comm, l->comm_stream);
+        if (r != ncclSuccess) return fail(FI_ERR_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+        return FI_OK;
+    }
+    // the compute stream waits for every bucket before the optimizer reads the gradients
+    int join() {
+        l->buckets = n;
+        if (!l->comm || n == 0) return FI_OK;
+        FI_HIP_CHECK(hipEventRecord(l->comm_done, l->comm_stream));
+        FI_HIP_CHECK(hipStreamWaitEvent(l->stream, l->comm_done, 0));
+        return FI_OK;
+    }
+};
+
 static int mlp_forward(fi_learner* l) {
     const int D = l->D, H = l->H, A = l->A;
     const float* W1 = l->params;
@@ -427,7 +470,7 @@ static int wgrad(fi_learner* l, const char* tag, const float* X, int I, const fl
     return FI_OK;
 }
 
-static int mlp_backward(fi_learner* l) {
+static int mlp_backward(fi_learner* l, GradReadyHook* gr) {
     const int D = l->D, H = l->H, A = l->A, O = A + 1;
     const float* W2 = l->params + (size_t)D * H + H;
     const float* Wh = W2 + (size_t)H * H + H;
@@ -442,10 +485,13 @@ static int mlp_backward(fi_learner* l) {
     { Tag t(l, "mlp_wgrad_heads"); FI_TRY(f32_heads_wgrad_partial(l->h2, H, g, l->splits, l->slab, cs, l->stream)); }
     { Tag t(l, "reduce_slabs"); FI_TRY(reduce_slabs(l->slab, l->splits, (size_t)H * O, gWh, l->stream)); }
     { Tag t(l, "reduce_slabs"); FI_TRY(reduce_slabs(cs, l->splits, (size_t)O, gbh, l->stream)); }
+    FI_TRY(gr->ready((size_t)(gWh - l->grads), (size_t)H * O + O));
     { Tag t(l, "mlp_dgrad_heads"); FI_TRY(f32_heads_dgrad(g, Wh, H, l->h2, l->dz2, l->stream)); }
     FI_TRY(wgrad(l, "mlp_wgrad_l2", l->h1, H, l->dz2, H, gW2, gb2));
+    FI_TRY(gr->ready((size_t)(gW2 - l->grads), (size_t)H * H + H));
     { Tag t(l, "mlp_dgrad_l2"); FI_TRY(f32_linear_dgrad(l->dz2, l->rows, H, W2, H, l->h1, l->dz1, l->stream)); }
     FI_TRY(wgrad(l, "mlp_wgrad_l1", l->obs, D, l->dz1, H, gW1, gb1));
+    FI_TRY(gr->ready(0, (size_t)D * H + H));
     return FI_OK;
 }
 
@@ -513,19 +559,19 @@ static int run_step(fi_learner* l, bool have_host_batch, fi_step_stats* out) {
                              l->bad));
     }
     mark(l, FI_PHASE_BACKWARD);
-    if (l->cfg.arch == FI_ARCH_MLP) FI_TRY(mlp_backward(l));
+    BucketAllReduce bar(l);
+    if (l->cfg.arch == FI_ARCH_MLP) FI_TRY(mlp_backward(l, &bar));
     else {
         LearnerTagger tg(l);
         FI_TRY(atari_backward(l->atari, l->frames, l->dlogits, l->dvalue, l->grads, l->stream,
-                              l->profiling ? &tg : nullptr));
+                              l->profiling ? &tg : nullptr, &bar));
     }
+    // the "allreduce" phase is the exposed tail: the wait for the buckets still in flight
+    // when the backward has finished
     mark(l, FI_PHASE_ALLREDUCE);
-    if (l->comm) {
-        Tag t(l, "allreduce");
-        ncclResult_t r = ncclAllReduce(l->grads, l->grads, l->nparams, ncclFloat, ncclSum, l->comm,
-                                       l->stream);
-        if (r != ncclSuccess)
-            return fail(FI_ERR_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+    {
+        Tag t(l, "allreduce_wait");
+        FI_TRY(bar.join());
     }
     mark(l, FI_PHASE_OPTIMIZER);
     {
@@ -898,6 +944,12 @@ extern "C" int fi_learner_load_state(fi_learner* l, const void* src, size_t byte
 }
 
 // ------------------------------------------------------------------ data parallel
+static int ensure_comm_stream(fi_learner* l) {
+    if (!l->comm_stream) FI_HIP_CHECK(hipStreamCreateWithFlags(&l->comm_stream, hipStreamNonBlocking));
+    if (!l->comm_done) FI_HIP_CHECK(hipEventCreateWithFlags(&l->comm_done, hipEventDisableTiming));
+    return FI_OK;
+}
+
 extern "C" int fi_comm_unique_id_bytes(void) { return (int)sizeof(ncclUniqueId); }
 
 extern "C" int fi_comm_get_unique_id(void* dst, size_t bytes) {
@@ -923,10 +975,69 @@ extern "C" int fi_learner_attach_comm(fi_learner* l, const void* uid, size_t byt
     if (nranks == 1 && !std::getenv("FI_COMM_SINGLE")) return FI_OK;
     ncclUniqueId id;
     std::memcpy(&id, uid, sizeof(id));
+    FI_TRY(ensure_comm_stream(l));
     ncclResult_t r = ncclCommInitRank(&l->comm, nranks, id, rank);
     if (r != ncclSuccess) return fail(FI_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
     l->rank = rank;
     l->nranks = nranks;
+    return FI_OK;
+}
+
+// One process driving several devices (one handle per device, e.g. the threaded
+// cmd/freeimpala with --devices 0,1,...): the per-device ncclCommInitRank calls are one group,
+// so a single thread can attach them all (called one by one, the first would block waiting
+// for its peers). Handle i becomes rank i of n.
+extern "C" int fi_comm_init_all(fi_learner* const* handles, int n) {
+    FI_REQUIRE(handles && n >= 1, "comm_init_all: bad arguments");
+    for (int i = 0; i < n; ++i) {
+        FI_REQUIRE(handles[i], "comm_init_all: null handle");
+        for (int j = 0; j < i; ++j)
+            FI_REQUIRE(handles[j]->dev != handles[i]->dev, "comm_init_all: two handles on one device");
+    }
+    if (n == 1 && !std::getenv("FI_COMM_SINGLE")) return FI_OK;
+    ncclUniqueId id;
+    ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) return fail(FI_ERR_COMM, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+    for (int i = 0; i < n; ++i) {
+        fi_learner* l = handles[i];
+        FI_HIP_CHECK(hipSetDevice(l->dev));
+        if (l->comm) {
+            ncclCommDestroy(l->comm);
+            l->comm = nullptr;
+        }
+        FI_TRY(ensure_comm_stream(l));
+    }
+    r = ncclGroupStart();
+    if (r != ncclSuccess) return fail(FI_ERR_COMM, std::string("ncclGroupStart: ") + ncclGetErrorString(r));
+    for (int i = 0; i < n; ++i) {
+        FI_HIP_CHECK(hipSetDevice(handles[i]->dev));
+        r = ncclCommInitRank(&handles[i]->comm, n, id, i);
+        if (r != ncclSuccess) {
+            ncclGroupEnd();
+            return fail(FI_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+        }
+    }
+    r = ncclGroupEnd();
+    if (r != ncclSuccess) return fail(FI_ERR_COMM, std::string("ncclGroupEnd: ") + ncclGetErrorString(r));
+    for (int i = 0; i < n; ++i) {
+        handles[i]->rank = i;
+        handles[i]->nranks = n;
+    }
+    return FI_OK;
+}
+
+// what RCCL reports for the handle's communicator (1 / 0 / 0 without one)
+extern "C" int fi_learner_comm_info(fi_learner* l, int* nranks, int* rank, int* buckets) {
+    FI_REQUIRE(l, "comm_info: null learner");
+    int n = 1, r = 0;
+    if (l->comm) {
+        ncclResult_t e = ncclCommCount(l->comm, &n);
+        if (e == ncclSuccess) e = ncclCommUserRank(l->comm, &r);
+        if (e != ncclSuccess) return fail(FI_ERR_COMM, std::string("ncclCommCount: ") + ncclGetErrorString(e));
+    }
+    if (nranks) *nranks = n;
+    if (rank) *rank = r;
+    if (buckets) *buckets = l->comm ? l->buckets : 0;
     return FI_OK;
 }
 

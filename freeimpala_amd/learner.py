@@ -226,6 +226,18 @@ class DeviceLearner:
     def attach_comm(self, uid: bytes, rank: int, nranks: int) -> None:
         check(lib().fi_learner_attach_comm(self._h, uid, len(uid), rank, nranks), "attach_comm")
 
+    def comm_info(self) -> dict:
+        """RCCL's view of this handle's communicator and the gradient buckets of its last step."""
+        n, r, b = C.c_int(), C.c_int(), C.c_int()
+        check(lib().fi_learner_comm_info(self._h, C.byref(n), C.byref(r), C.byref(b)), "comm_info")
+        return {"nranks": n.value, "rank": r.value, "buckets_last_step": b.value}
+
+    @staticmethod
+    def comm_init_all(learners) -> None:
+        """One process, several devices: all handles join one communicator (rank = list index)."""
+        arr = (C.c_void_p * len(learners))(*[x._h for x in learners])
+        check(lib().fi_comm_init_all(arr, len(learners)), "comm_init_all")
+
     # --- profiling
     def set_profiling(self, on: bool) -> None:
         check(lib().fi_learner_set_profiling(self._h, int(on)), "set_profiling")

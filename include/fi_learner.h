@@ -143,6 +143,14 @@ int fi_comm_unique_id_bytes(void);
 int fi_comm_get_unique_id(void* dst, size_t bytes);
 int fi_learner_attach_comm(fi_learner* l, const void* unique_id, size_t bytes, int rank,
                            int nranks);
+/* One process, several devices: handle i (each on its own device) becomes rank i of n; the
+ * per-device communicator inits run as one RCCL group, so one thread can call this (the
+ * one-rank-per-process form above blocks until every peer has joined).                    */
+int fi_comm_init_all(fi_learner* const* handles, int n);
+/* The handle's communicator as RCCL reports it (ncclCommCount / ncclCommUserRank; 1 / 0
+ * without one) and the gradient buckets its last step all-reduced (reverse layer order,
+ * overlapped with the backward on a second stream).                                        */
+int fi_learner_comm_info(fi_learner* l, int* nranks, int* rank, int* buckets);
 
 /* ---- introspection for tests / bench ------------------------------------------------
  * fi_learner_tensor: device pointer + bytes of a named internal tensor ("params", "grads",

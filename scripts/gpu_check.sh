@@ -11,7 +11,7 @@ TAG=${TAG:-r01}
 fatal() { case $1 in 0|1) return 1;; *) echo "fatal rc=$1 in $2"; exit "$1";; esac; }
 
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
-  timeout -k 10 ${TEST_TIMEOUT:-900} python -m pytest tests -q -m gpu ${PYTEST_ARGS:--x} --timeout=300 \
+  timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest tests -v -m gpu ${PYTEST_ARGS:--x} --timeout=300 --timeout-method thread \
       > "$OUT/pytest_gpu_$TAG.log" 2>&1
   rc=$?; echo "pytest rc=$rc"; tail -5 "$OUT/pytest_gpu_$TAG.log"
   fatal $rc pytest || true

@@ -129,9 +129,11 @@ def test_config1_end_to_end_vs_oracle_and_resume(orc, tmp_path):
         assert l2 < 2e-3, (k, l2)
         p = p1
     np.testing.assert_array_equal(latest[8:].view(np.float32), p)
-    # resume: --starting-model picks model_0_latest.bin + its .state; publication continues at 5
+    # resume: --starting-model picks model_0_latest.bin + its .state; publication continues at 5.
+    # --iterations 64 with 4 agents and M = 32 -> floor(4 * 64 / 32) = 8 learner iterations; the
+    # count restarts at 0 after a resume, as in the reference (learner.h:73)
     dump2 = tmp_path / "dump2"
-    r = run(CONFIG1[:2] + ["--iterations", "8"] + CONFIG1[4:] + common[:4] + ["--checkpoint-location", str(tmp_path / "ck2")]
+    r = run(CONFIG1[:2] + ["--iterations", "64"] + CONFIG1[4:] + common[:4] + ["--checkpoint-location", str(tmp_path / "ck2")]
             + common[6:] + ["--starting-model", str(ck), "--dump-dir", str(dump2)])
     assert r.returncode == 0, r.stdout + r.stderr
     assert "resumed learner state" in r.stderr

@@ -30,11 +30,13 @@ def grads_close(a, b, what="", rel_l2=1e-5, rel_max=3e-4):
     assert l2 <= rel_l2 and mx <= rel_max, f"{what}: rel L2 {l2:.2e}, rel max {mx:.2e}"
 
 
-def mk(T=5, B=16, A=18, D=128, H=256, **kw):
+def mk(T=5, B=16, A=18, D=128, H=256, arch="mlp", **kw):
     from freeimpala_amd.learner import DeviceLearner
     kw.setdefault("optimizer", "sgd")
     kw.setdefault("lr", 1e-3)
     kw.setdefault("max_grad_norm", 0.0)
+    if arch != "mlp":
+        return DeviceLearner(arch, seq_len=T, batch=B, num_actions=A, **kw)
     return DeviceLearner("mlp", seq_len=T, batch=B, num_actions=A, obs_dim=D, hidden=H, **kw)
 
 
@@ -246,16 +248,27 @@ def test_staged_steps_match_entry_steps(orc):
     assert s1["total_loss"] == s2["total_loss"] and s1["version"] == s2["version"] == 5
 
 
-def test_rccl_one_rank_allreduce_step_matches(monkeypatch):
+@pytest.mark.parametrize("arch", ["mlp", "atari"])
+@pytest.mark.parametrize("attach", ["uid", "init_all"])
+def test_rccl_one_rank_allreduce_step_matches(monkeypatch, arch, attach):
     """The data-parallel path on one GPU: a handle attached to a one-rank RCCL communicator
-    (FI_COMM_SINGLE) runs the in-step ncclAllReduce(sum) of the flat gradient on its stream;
-    a one-rank sum is the identity, so its parameters after three Adam steps equal those of a
-    handle without a communicator, bit for bit. Covers unique id / attach / all-reduce /
-    teardown; N > 1 needs several GPUs (RCCL refuses two ranks on one device)."""
+    (FI_COMM_SINGLE) runs the bucketed in-step ncclAllReduce(sum) of the gradient (3 buckets,
+    reverse layer order, on the comm stream overlapped with the backward); a one-rank sum is
+    the identity, so its parameters after three Adam steps equal those of a handle without a
+    communicator, bit for bit. Covers unique id / attach (one-rank-per-process form and the
+    grouped single-process fi_comm_init_all) / all-reduce / teardown, and RCCL's own view of
+    the communicator; N > 1 needs several GPUs (RCCL refuses two ranks on one device)."""
     from freeimpala_amd.learner import DeviceLearner
     monkeypatch.setenv("FI_COMM_SINGLE", "1")
-    L1, L2 = mk(T=4, B=32, seed=5, optimizer="adam"), mk(T=4, B=32, seed=5, optimizer="adam")
-    L2.attach_comm(DeviceLearner.comm_unique_id(), 0, 1)
+    kw = dict(T=4, B=32, seed=5, optimizer="adam")
+    if arch == "atari":
+        kw = dict(T=2, B=16, seed=5, optimizer="adam")
+    L1, L2 = mk(arch=arch, **kw), mk(arch=arch, **kw)
+    if attach == "uid":
+        L2.attach_comm(DeviceLearner.comm_unique_id(), 0, 1)
+    else:
+        DeviceLearner.comm_init_all([L2])
+    assert L1.comm_info()["nranks"] == 1
     s = {}
     for i, L in enumerate((L1, L2)):
         L.synth(seed=12)
@@ -263,6 +276,8 @@ def test_rccl_one_rank_allreduce_step_matches(monkeypatch):
             s[i] = L.step_resident()
     np.testing.assert_array_equal(L1.get_params(), L2.get_params())
     assert s[0]["total_loss"] == s[1]["total_loss"]
+    assert L2.comm_info() == {"nranks": 1, "rank": 0, "buckets_last_step": 3}
+    assert L1.comm_info()["buckets_last_step"] == 0
     L1.close()
     L2.close()
 
@@ -296,7 +311,7 @@ def test_out_of_range_action_rejects_batch(orc):
     from freeimpala_amd.learner import pack_records
     T, B = 4, 32
     good = orc.synth_batch(41, T=T, B=B, A=18, D=128)
-    bad = {k: v.copy() for k, v in good.items()}
+    bad = {k: (None if v is None else v.copy()) for k, v in good.items()}
     bad["actions"][2, 5] = 18
     bad["actions"][0, 0] = -1
     with pytest.raises(Exception):
