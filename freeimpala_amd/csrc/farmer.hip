@@ -1,0 +1,605 @@
+// farmer.hip -- FarmerLstmModel train step on gfx950 behind include/fi_farmer.h.
+//
+// The reference's only network and its supervised step (scripts/gpu_benchmark.py:11-44,
+// 46-66, 99-125; cmd/libtorch_bench/main.cpp:14-42, 117-135), rebuilt for MI355X in fp32
+// (the reference's precision):
+//   input projection  XP[B*T][512] = z W_ih^T + (b_ih + b_hh)      one MFMA GEMM (gemm_f32.hip)
+//   recurrence        lstm_fwd_kernel: one workgroup per 8 batch rows walks t = 0..T-1; the
+//                     rows' h_{t-1} sits in LDS ([k][row], broadcast float4 reads), W_hh^T
+//                     streams from L1/L2 (coalesced rows of the transposed copy), c in
+//                     registers; packed-fp32 FMAs; gates i, f, g, o in PyTorch order
+//   torso             cat(h_T, x) -> 5 x (Linear 512 + ReLU) -> Linear 512 -> 1 (MFMA GEMMs
+//                     with bias+ReLU epilogues; the last layer a per-row dot)
+//   criterion         mse / mae / huber mean + its gradient, one deterministic block
+//   backward          dense layers: weight-gradient GEMMs into split-K slabs reduced in a
+//                     fixed order, ReLU-masked data gradients; BPTT: lstm_bwd_kernel walks
+//                     t = T-1..0 per 8 rows (dc in registers, dgates to HBM and LDS, dh_{t-1} =
+//                     dgates W_hh from LDS-broadcast dgates x coalesced W_hh rows); W_ih / W_hh
+//                     gradients = two GEMMs over all B*T rows; bias = column sums
+//   optimizer         torch.optim.Adam / AdamW / SGD update formulas (single-tensor forms) in fp32
+// Everything is deterministic (no float atomics). One HIP stream per handle.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "fi_common.h"
+#include "fi_farmer.h"
+#include "kernels.h"
+
+namespace fi {
+namespace farmer {
+
+constexpr int IN = 162, H = 128, G = 4 * H, XD = 484, CAT = H + XD, DW = 512;
+constexpr int RB = 8;  // batch rows per recurrence workgroup
+
+struct Off {
+    size_t wih, whh, bih, bhh, w[7], b[7], total;
+    Off() {
+        size_t o = 0;
+        wih = o; o += (size_t)G * IN;
+        whh = o; o += (size_t)G * H;
+        bih = o; o += G;
+        bhh = o; o += G;
+        w[0] = b[0] = 0;
+        for (int l = 1; l <= 6; ++l) {
+            const int in = l == 1 ? CAT : DW, out = l == 6 ? 1 : DW;
+            w[l] = o; o += (size_t)out * in;
+            b[l] = o; o += out;
+        }
+        total = o;
+    }
+};
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float sigm(float a) { return 1.0f / (1.0f + __expf(-a)); }
+
+// WT[k][n] = W_hh[n][k] (the recurrence reads rows of W_hh^T, coalesced across units);
+// bsum = b_ih + b_hh
+__global__ void lstm_prep_kernel(const float* __restrict__ whh, const float* __restrict__ bih,
+                                 const float* __restrict__ bhh, float* __restrict__ wt, float* __restrict__ bsum) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < G * H) {
+        const int n = i / H, k = i - n * H;
+        wt[(size_t)k * G + n] = whh[i];
+    }
+    if (i < G) bsum[i] = bih[i] + bhh[i];
+}
+
+// Forward recurrence. Thread (u, rh): hidden unit u, rows 4rh..4rh+3 of the workgroup's 8;
+// 16 gate accumulators (i, f, g, o x 4 rows) as packed pairs. Stores, per (row, t): gates
+// (post-activation) [B*T][512], c [B*T][128], h_{t-1} [B*T][128] (the W_hh gradient's
+// operand); h_T into cat[:, 0:128].
+__global__ __launch_bounds__(256) void lstm_fwd_kernel(const float* __restrict__ xp, const float* __restrict__ wt,
+                                                       int B, int T, float* __restrict__ gates,
+                                                       float* __restrict__ cst, float* __restrict__ hprev,
+                                                       float* __restrict__ cat) {
+    __shared__ __attribute__((aligned(16))) float hT[H][RB];
+    const int u = threadIdx.x & (H - 1), rh = threadIdx.x >> 7;
+    const int b0 = blockIdx.x * RB + 4 * rh;
+    float c[4], h[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        c[j] = 0.f;
+        h[j] = 0.f;
+        hT[u][4 * rh + j] = 0.f;
+    }
+    __syncthreads();
+    for (int t = 0; t < T; ++t) {
+        f32x2 acc[4][2];  // [gate][row pair]
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                float v[2];
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const int row = b0 + 2 * p + q;
+                    v[q] = row < B ? xp[((size_t)row * T + t) * G + g * H + u] : 0.f;
+                }
+                acc[g][p] = f32x2{v[0], v[1]};
+            }
+        const float* wk = wt + u;
+#pragma unroll 4
+        for (int k = 0; k < H; ++k) {
+            const f32x4v hv = *(const f32x4v*)&hT[k][4 * rh];
+            const f32x2 h01 = {hv.x, hv.y}, h23 = {hv.z, hv.w};
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const float w = wk[(size_t)k * G + g * H];
+                const f32x2 w2 = {w, w};
+                acc[g][0] = __builtin_elementwise_fma(w2, h01, acc[g][0]);
+                acc[g][1] = __builtin_elementwise_fma(w2, h23, acc[g][1]);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int p = j >> 1, q = j & 1;
+            const float ig = sigm(acc[0][p][q]), fg = sigm(acc[1][p][q]);
+            const float gg = tanhf(acc[2][p][q]), og = sigm(acc[3][p][q]);
+            const float hp = h[j];
+            c[j] = fg * c[j] + ig * gg;
+            h[j] = og * tanhf(c[j]);
+            const int row = b0 + j;
+            if (row < B) {
+                const size_t e = (size_t)row * T + t;
+                float* gr = gates + e * G + u;
+                gr[0] = ig;
+                gr[H] = fg;
+                gr[2 * H] = gg;
+                gr[3 * H] = og;
+                cst[e * H + u] = c[j];
+                hprev[e * H + u] = hp;
+                if (t == T - 1) cat[(size_t)row * CAT + u] = h[j];
+            }
+        }
+        __syncthreads();  // every thread has read hT for step t
+#pragma unroll
+        for (int j = 0; j < 4; ++j) hT[u][4 * rh + j] = h[j];
+        __syncthreads();
+    }
+}
+
+// Backward recurrence (BPTT). dh_T = dcat[:, 0:128]; per step t = T-1..0, thread (u, rh):
+//   do = dh tanh(c_t); dc += dh o (1 - tanh^2 c_t); di = dc g; dg = dc i; df = dc c_{t-1}
+//   pre-activation grads (i, f, g, o) -> dG[B*T][512] (HBM) and dGT[512][8] (LDS)
+//   dc <- dc f;  dh_{t-1}[row][u] = sum_n dG[row][n] W_hh[n][u]
+__global__ __launch_bounds__(256) void lstm_bwd_kernel(const float* __restrict__ gates, const float* __restrict__ cst,
+                                                       const float* __restrict__ whh, const float* __restrict__ dcat,
+                                                       int B, int T, float* __restrict__ dG) {
+    __shared__ __attribute__((aligned(16))) float dGT[G][RB];
+    const int u = threadIdx.x & (H - 1), rh = threadIdx.x >> 7;
+    const int b0 = blockIdx.x * RB + 4 * rh;
+    float dh[4], dc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int row = b0 + j;
+        dh[j] = row < B ? dcat[(size_t)row * CAT + u] : 0.f;
+        dc[j] = 0.f;
+    }
+    for (int t = T - 1; t >= 0; --t) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int row = b0 + j;
+            float dgi = 0.f, dgf = 0.f, dgg = 0.f, dgo = 0.f;
+            if (row < B) {
+                const size_t e = (size_t)row * T + t;
+                const float* gr = gates + e * G + u;
+                const float ig = gr[0], fg = gr[H], gg = gr[2 * H], og = gr[3 * H];
+                const float ct = cst[e * H + u];
+                const float cp = t > 0 ? cst[(e - 1) * H + u] : 0.f;
+                const float tc = tanhf(ct);
+                const float d_o = dh[j] * tc;
+                dc[j] += dh[j] * og * (1.f - tc * tc);
+                const float di = dc[j] * gg, dgv = dc[j] * ig, df = dc[j] * cp;
+                dgi = di * ig * (1.f - ig);
+                dgf = df * fg * (1.f - fg);
+                dgg = dgv * (1.f - gg * gg);
+                dgo = d_o * og * (1.f - og);
+                dc[j] *= fg;
+                float* dr = dG + e * G + u;
+                dr[0] = dgi;
+                dr[H] = dgf;
+                dr[2 * H] = dgg;
+                dr[3 * H] = dgo;
+            }
+            dGT[u][4 * rh + j] = dgi;
+            dGT[H + u][4 * rh + j] = dgf;
+            dGT[2 * H + u][4 * rh + j] = dgg;
+            dGT[3 * H + u][4 * rh + j] = dgo;
+        }
+        __syncthreads();
+        if (t > 0) {
+            f32x2 a01 = {0.f, 0.f}, a23 = {0.f, 0.f};
+            const float* wc = whh + u;
+#pragma unroll 8
+            for (int n = 0; n < G; ++n) {
+                const f32x4v g4 = *(const f32x4v*)&dGT[n][4 * rh];
+                const float w = wc[(size_t)n * H];
+                const f32x2 w2 = {w, w};
+                a01 = __builtin_elementwise_fma(w2, f32x2{g4.x, g4.y}, a01);
+                a23 = __builtin_elementwise_fma(w2, f32x2{g4.z, g4.w}, a23);
+            }
+            dh[0] = a01.x;
+            dh[1] = a01.y;
+            dh[2] = a23.x;
+            dh[3] = a23.y;
+        }
+        __syncthreads();  // dGT is rewritten next step
+    }
+}
+
+// cat[b][128:612] = x[b]
+__global__ void cat_x_kernel(const float* __restrict__ x, int B, float* __restrict__ cat) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B * XD) return;
+    const int b = i / XD, k = i - b * XD;
+    cat[(size_t)b * CAT + H + k] = x[i];
+}
+
+// value[b] = a5[b] . w6 + b6: one wave per row
+__global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__ a5, const float* __restrict__ w6,
+                                                       const float* __restrict__ b6, int B, float* __restrict__ val) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= B) return;
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < DW / 64; ++i) s = fmaf(a5[(size_t)row * DW + lane + 64 * i], w6[lane + 64 * i], s);
+    s = wave_sum(s);
+    if (lane == 0) val[row] = s + b6[0];
+}
+
+// criterion (mean over B) and dL/dvalue; one block, double accumulation in a fixed order
+__global__ __launch_bounds__(256) void loss_kernel(const float* __restrict__ val, const float* __restrict__ y, int B,
+                                                   int kind, float* __restrict__ dval, double* __restrict__ loss) {
+    __shared__ double red[4];
+    double s = 0.0;
+    const float invn = 1.0f / (float)B;
+    for (int b = threadIdx.x; b < B; b += 256) {
+        const float d = val[b] - y[b];
+        const float ad = fabsf(d);
+        float l, gd;
+        if (kind == FI_LOSS_MSE) {
+            l = d * d;
+            gd = (2.0f * invn) * d;  // torch mse_loss_backward: (2 / N) * (x - y)
+        } else if (kind == FI_LOSS_MAE) {
+            l = ad;
+            gd = (d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f)) * invn;
+        } else {  // SmoothL1Loss, beta = 1
+            l = ad < 1.f ? 0.5f * d * d : ad - 0.5f;
+            gd = (d < -1.f ? -1.f : (d > 1.f ? 1.f : d)) * invn;
+        }
+        dval[b] = gd;
+        s += (double)l;
+    }
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) *loss = ((red[0] + red[1]) + (red[2] + red[3])) / (double)B;
+}
+
+// dense6 backward: dW6[k] = sum_b dval[b] a5[b][k] (fixed order), db6 = sum_b dval[b],
+// da5[b][k] = (a5 > 0) dval[b] w6[k]
+__global__ __launch_bounds__(DW) void head_bwd_kernel(const float* __restrict__ a5, const float* __restrict__ w6,
+                                                      const float* __restrict__ dval, int B, float* __restrict__ gw6,
+                                                      float* __restrict__ gb6, float* __restrict__ da5) {
+    const int k = threadIdx.x;
+    float s = 0.f, sb = 0.f;
+    const float wk = w6[k];
+    for (int b = 0; b < B; ++b) {
+        const float a = a5[(size_t)b * DW + k], d = dval[b];
+        s = fmaf(d, a, s);
+        sb += d;
+        da5[(size_t)b * DW + k] = a > 0.f ? d * wk : 0.f;
+    }
+    gw6[k] = s;
+    if (k == 0) *gb6 = sb;
+}
+
+// b_ih and b_hh receive the same gradient (column sums of dG)
+__global__ void copy_kernel(const float* __restrict__ src, float* __restrict__ dst, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = src[i];
+}
+
+// torch.optim single-tensor update formulas in fp32 (torch/optim/adam.py, sgd.py):
+//   AdamW: p *= 1 - lr wd;  m = lerp(m, g, 1 - b1);  v = v b2 + (1 - b2) g g
+//   p += -(lr / bc1) m / (sqrt(v) / sqrt(bc2) + eps);   Adam with wd: g += wd p first;  SGD: p += -lr g
+__global__ void farmer_opt_kernel(int kind, float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                                  float* __restrict__ v, size_t n, float lr, float wd, float b1, float b2, float eps,
+                                  float neg_step_size, float bc2_sqrt, float decay) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        float pi = p[i], gi = g[i];
+        if (kind == FI_FOPT_SGD) {
+            p[i] = __fadd_rn(pi, __fmul_rn(-lr, gi));
+            continue;
+        }
+        if (kind == FI_FOPT_ADAMW) pi = __fmul_rn(pi, decay);
+        else if (wd != 0.f) gi = __fadd_rn(gi, __fmul_rn(wd, pi));
+        const float w = 1.0f - b1;
+        const float mi = __fadd_rn(m[i], __fmul_rn(w, __fsub_rn(gi, m[i])));
+        const float vi = __fadd_rn(__fmul_rn(v[i], b2), __fmul_rn(__fmul_rn(1.0f - b2, gi), gi));
+        m[i] = mi;
+        v[i] = vi;
+        const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(vi), bc2_sqrt), eps);
+        p[i] = __fadd_rn(pi, __fdiv_rn(__fmul_rn(neg_step_size, mi), denom));
+    }
+}
+
+}  // namespace farmer
+}  // namespace fi
+
+using namespace fi;
+using namespace fi::farmer;
+
+struct fi_farmer {
+    fi_farmer_config cfg{};
+    int dev = 0;
+    hipStream_t stream = nullptr;
+    int B = 0, T = 0;
+    Off off;
+    uint64_t step = 0;
+    float *params = nullptr, *grads = nullptr, *m = nullptr, *v = nullptr;
+    float *wt = nullptr, *bsum = nullptr;
+    float *z = nullptr, *x = nullptr, *y = nullptr;                   // resident input buffers
+    float *xp = nullptr, *gates = nullptr, *cst = nullptr, *hprev = nullptr, *dG = nullptr;
+    float *cat = nullptr, *act[6] = {}, *val = nullptr, *dval = nullptr, *dcat = nullptr;
+    float *dA = nullptr, *dB = nullptr;
+    float *slab = nullptr;
+    size_t slab_floats = 0;
+    double* loss = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    std::vector<void*> allocs;
+};
+
+static int falloc(fi_farmer* f, float** p, size_t n) {
+    void* q = nullptr;
+    hipError_t e = hipMalloc(&q, std::max<size_t>(n, 4) * sizeof(float));
+    if (e != hipSuccess) return fail(FI_ERR_OOM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    f->allocs.push_back(q);
+    *p = (float*)q;
+    return FI_OK;
+}
+
+static int splits_for(int M) { return std::max(1, std::min(16, M / 256)); }
+
+// weight gradient [N][K] of a layer (PyTorch layout) + its bias gradient, deterministic
+static int wgrad(fi_farmer* f, const float* dY, int M, int N, const float* X, int ldx, int K, float* gW, float* gb) {
+    const int sp = splits_for(M);
+    FI_REQUIRE((size_t)sp * N * K <= f->slab_floats, "farmer: slab too small");
+    FI_TRY(f32_gemm_tn_wgrad(dY, M, N, X, ldx, K, sp, f->slab, f->stream));
+    FI_TRY(reduce_slabs(f->slab, sp, (size_t)N * K, gW, f->stream));
+    if (gb) {
+        const int cs = std::max(1, std::min(64, M / 64));
+        FI_TRY(colsum_partial(dY, M, N, cs, f->slab, f->stream));
+        FI_TRY(reduce_slabs(f->slab, cs, (size_t)N, gb, f->stream));
+    }
+    return FI_OK;
+}
+
+static int forward(fi_farmer* f) {
+    hipStream_t s = f->stream;
+    const int B = f->B, T = f->T;
+    const Off& o = f->off;
+    float* P = f->params;
+    hipLaunchKernelGGL(lstm_prep_kernel, dim3((G * H + 255) / 256), dim3(256), 0, s, P + o.whh, P + o.bih, P + o.bhh,
+                       f->wt, f->bsum);
+    FI_TRY(f32_gemm_nt(f->z, IN, B * T, IN, P + o.wih, f->bsum, G, false, f->xp, s));
+    hipLaunchKernelGGL(lstm_fwd_kernel, dim3((B + RB - 1) / RB), dim3(256), 0, s, f->xp, f->wt, B, T, f->gates, f->cst,
+                       f->hprev, f->cat);
+    hipLaunchKernelGGL(cat_x_kernel, dim3((B * XD + 255) / 256), dim3(256), 0, s, f->x, B, f->cat);
+    const float* in = f->cat;
+    int K = CAT;
+    for (int l = 1; l <= 5; ++l) {
+        FI_TRY(f32_gemm_nt(in, K, B, K, P + o.w[l], P + o.b[l], DW, true, f->act[l], s));
+        in = f->act[l];
+        K = DW;
+    }
+    hipLaunchKernelGGL(head_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, s, f->act[5], P + o.w[6], P + o.b[6], B, f->val);
+    FI_HIP_CHECK(hipGetLastError());
+    return FI_OK;
+}
+
+static int backward(fi_farmer* f) {
+    hipStream_t s = f->stream;
+    const int B = f->B, T = f->T;
+    const Off& o = f->off;
+    float* P = f->params;
+    float* Gd = f->grads;
+    hipLaunchKernelGGL(loss_kernel, dim3(1), dim3(256), 0, s, f->val, f->y, B, f->cfg.loss, f->dval, f->loss);
+    hipLaunchKernelGGL(head_bwd_kernel, dim3(1), dim3(DW), 0, s, f->act[5], P + o.w[6], f->dval, B, Gd + o.w[6],
+                       Gd + o.b[6], f->dA);
+    float* dcur = f->dA;
+    float* dnext = f->dB;
+    for (int l = 5; l >= 1; --l) {
+        const float* X = l == 1 ? f->cat : f->act[l - 1];
+        const int K = l == 1 ? CAT : DW;
+        FI_TRY(wgrad(f, dcur, B, DW, X, K, K, Gd + o.w[l], Gd + o.b[l]));
+        if (l > 1) {
+            FI_TRY(f32_gemm_nn_dgrad(dcur, B, DW, P + o.w[l], DW, f->act[l - 1], dnext, s));
+            std::swap(dcur, dnext);
+        } else {
+            FI_TRY(f32_gemm_nn_dgrad(dcur, B, DW, P + o.w[1], CAT, nullptr, f->dcat, s));
+        }
+    }
+    hipLaunchKernelGGL(lstm_bwd_kernel, dim3((B + RB - 1) / RB), dim3(256), 0, s, f->gates, f->cst, P + o.whh, f->dcat,
+                       B, T, f->dG);
+    FI_TRY(wgrad(f, f->dG, B * T, G, f->z, IN, IN, Gd + o.wih, Gd + o.bih));
+    FI_TRY(wgrad(f, f->dG, B * T, G, f->hprev, H, H, Gd + o.whh, nullptr));
+    hipLaunchKernelGGL(copy_kernel, dim3((G + 255) / 256), dim3(256), 0, s, Gd + o.bih, Gd + o.bhh, G);
+    FI_HIP_CHECK(hipGetLastError());
+    return FI_OK;
+}
+
+static int optimize(fi_farmer* f) {
+    const fi_farmer_config& c = f->cfg;
+    f->step++;
+    // the host-side scalars exactly as torch computes them (Python doubles, used as fp32)
+    const double bc1 = 1.0 - std::pow((double)c.beta1, (double)f->step);
+    const double bc2 = 1.0 - std::pow((double)c.beta2, (double)f->step);
+    const float neg_ss = (float)(-((double)c.lr / bc1));
+    const float bc2s = (float)std::sqrt(bc2);
+    const float decay = (float)(1.0 - (double)c.lr * (double)c.weight_decay);
+    const size_t n = f->off.total;
+    hipLaunchKernelGGL(farmer_opt_kernel, dim3(1024), dim3(256), 0, f->stream, c.optimizer, f->params, f->grads, f->m,
+                       f->v, n, c.lr, c.weight_decay, c.beta1, c.beta2, c.eps, neg_ss, bc2s, decay);
+    FI_HIP_CHECK(hipGetLastError());
+    return FI_OK;
+}
+
+static int stage_inputs(fi_farmer* f, const float* z, const float* x, const float* y, int on_device) {
+    const size_t nz = (size_t)f->B * f->T * IN, nx = (size_t)f->B * XD, ny = (size_t)f->B;
+    const hipMemcpyKind k = on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    if (z && z != f->z) FI_HIP_CHECK(hipMemcpyAsync(f->z, z, nz * 4, k, f->stream));
+    if (x && x != f->x) FI_HIP_CHECK(hipMemcpyAsync(f->x, x, nx * 4, k, f->stream));
+    if (y && y != f->y) FI_HIP_CHECK(hipMemcpyAsync(f->y, y, ny * 4, k, f->stream));
+    return FI_OK;
+}
+
+extern "C" size_t fi_farmer_param_count(void) { return Off().total; }
+
+extern "C" void fi_farmer_config_init(fi_farmer_config* c) {
+    if (!c) return;
+    std::memset(c, 0, sizeof(*c));
+    c->batch = 32;  // gpu_benchmark.py:392-398 defaults
+    c->seq_len = 10;
+    c->loss = FI_LOSS_MSE;
+    c->optimizer = FI_FOPT_ADAM;
+    c->lr = 1e-3f;
+    c->beta1 = 0.9f;
+    c->beta2 = 0.999f;
+    c->eps = 1e-8f;
+    c->weight_decay = -1.f;  // < 0: torch's default for the optimizer (0 adam, 0.01 adamw)
+    c->device = 0;
+}
+
+extern "C" int fi_farmer_create(const fi_farmer_config* cfg, fi_farmer** out) {
+    FI_REQUIRE(cfg && out, "farmer_create: null argument");
+    *out = nullptr;
+    FI_REQUIRE(cfg->batch >= 1 && cfg->seq_len >= 1, "farmer_create: batch and seq_len must be >= 1");
+    FI_REQUIRE(cfg->loss >= 0 && cfg->loss <= 2, "farmer_create: loss must be mse (0), mae (1) or huber (2)");
+    FI_REQUIRE(cfg->optimizer >= 0 && cfg->optimizer <= 2, "farmer_create: optimizer must be adam, sgd or adamw");
+    FI_REQUIRE((size_t)cfg->batch * cfg->seq_len * G < ((size_t)1 << 31), "farmer_create: B*T*512 must stay < 2^31");
+    int ndev = 0;
+    FI_HIP_CHECK(hipGetDeviceCount(&ndev));
+    FI_REQUIRE(cfg->device >= 0 && cfg->device < ndev, "farmer_create: no such HIP device");
+    FI_HIP_CHECK(hipSetDevice(cfg->device));
+    fi_farmer* f = new fi_farmer();
+    f->cfg = *cfg;
+    if (f->cfg.weight_decay < 0.f) f->cfg.weight_decay = cfg->optimizer == FI_FOPT_ADAMW ? 0.01f : 0.f;
+    f->dev = cfg->device;
+    f->B = cfg->batch;
+    f->T = cfg->seq_len;
+    const size_t B = f->B, BT = (size_t)f->B * f->T, P = f->off.total;
+    int rc = FI_OK;
+    auto A = [&](float** p, size_t n) {
+        if (rc == FI_OK) rc = falloc(f, p, n);
+    };
+    A(&f->params, P); A(&f->grads, P); A(&f->m, P); A(&f->v, P);
+    A(&f->wt, (size_t)G * H); A(&f->bsum, G);
+    A(&f->z, BT * IN); A(&f->x, B * XD); A(&f->y, B);
+    A(&f->xp, BT * G); A(&f->gates, BT * G); A(&f->cst, BT * H); A(&f->hprev, BT * H); A(&f->dG, BT * G);
+    A(&f->cat, B * CAT); A(&f->dcat, B * CAT);
+    for (int l = 1; l <= 5; ++l) A(&f->act[l], B * DW);
+    A(&f->val, B); A(&f->dval, B); A(&f->dA, B * DW); A(&f->dB, B * DW);
+    f->slab_floats = std::max<size_t>((size_t)16 * G * IN, (size_t)16 * DW * CAT);
+    f->slab_floats = std::max<size_t>(f->slab_floats, (size_t)64 * G);
+    A(&f->slab, f->slab_floats);
+    float* lossf = nullptr;
+    A(&lossf, 2);
+    f->loss = (double*)lossf;
+    if (rc == FI_OK && hipStreamCreateWithFlags(&f->stream, hipStreamNonBlocking) != hipSuccess)
+        rc = fail(FI_ERR_HIP, "farmer_create: hipStreamCreate failed");
+    if (rc == FI_OK && (hipEventCreate(&f->e0) != hipSuccess || hipEventCreate(&f->e1) != hipSuccess))
+        rc = fail(FI_ERR_HIP, "farmer_create: hipEventCreate failed");
+    if (rc == FI_OK && (hipMemset(f->m, 0, P * 4) != hipSuccess || hipMemset(f->v, 0, P * 4) != hipSuccess ||
+                        hipMemset(f->params, 0, P * 4) != hipSuccess || hipMemset(f->grads, 0, P * 4) != hipSuccess ||
+                        hipMemset(f->z, 0, BT * IN * 4) != hipSuccess || hipMemset(f->x, 0, B * XD * 4) != hipSuccess ||
+                        hipMemset(f->y, 0, B * 4) != hipSuccess))
+        rc = fail(FI_ERR_HIP, "farmer_create: hipMemset failed");
+    if (rc != FI_OK) {
+        fi_farmer_destroy(f);
+        return rc;
+    }
+    *out = f;
+    return FI_OK;
+}
+
+extern "C" void fi_farmer_destroy(fi_farmer* f) {
+    if (!f) return;
+    hipSetDevice(f->dev);
+    if (f->stream) hipStreamSynchronize(f->stream);
+    for (void* p : f->allocs) hipFree(p);
+    if (f->e0) hipEventDestroy(f->e0);
+    if (f->e1) hipEventDestroy(f->e1);
+    if (f->stream) hipStreamDestroy(f->stream);
+    delete f;
+}
+
+extern "C" int fi_farmer_set_params(fi_farmer* f, const float* host, size_t n) {
+    FI_REQUIRE(f && host && n == f->off.total, "farmer_set_params: need fi_farmer_param_count() floats");
+    FI_HIP_CHECK(hipSetDevice(f->dev));
+    FI_HIP_CHECK(hipMemcpyAsync(f->params, host, n * 4, hipMemcpyHostToDevice, f->stream));
+    FI_HIP_CHECK(hipMemsetAsync(f->m, 0, n * 4, f->stream));
+    FI_HIP_CHECK(hipMemsetAsync(f->v, 0, n * 4, f->stream));
+    FI_HIP_CHECK(hipStreamSynchronize(f->stream));
+    f->step = 0;
+    return FI_OK;
+}
+
+static int d2h(fi_farmer* f, const float* src, float* host, size_t n) {
+    FI_HIP_CHECK(hipSetDevice(f->dev));
+    FI_HIP_CHECK(hipMemcpyAsync(host, src, n * 4, hipMemcpyDeviceToHost, f->stream));
+    FI_HIP_CHECK(hipStreamSynchronize(f->stream));
+    return FI_OK;
+}
+
+extern "C" int fi_farmer_get_params(fi_farmer* f, float* host, size_t n) {
+    FI_REQUIRE(f && host && n == f->off.total, "farmer_get_params: need fi_farmer_param_count() floats");
+    return d2h(f, f->params, host, n);
+}
+
+extern "C" int fi_farmer_get_grads(fi_farmer* f, float* host, size_t n) {
+    FI_REQUIRE(f && host && n == f->off.total, "farmer_get_grads: need fi_farmer_param_count() floats");
+    return d2h(f, f->grads, host, n);
+}
+
+extern "C" int fi_farmer_train_step(fi_farmer* f, const float* z, const float* x, const float* targets,
+                                    int inputs_on_device, float* values, fi_farmer_stats* out) {
+    FI_REQUIRE(f && z && x && targets, "farmer_train_step: null argument");
+    FI_HIP_CHECK(hipSetDevice(f->dev));
+    FI_TRY(stage_inputs(f, z, x, targets, inputs_on_device));
+    if (out) FI_HIP_CHECK(hipEventRecord(f->e0, f->stream));
+    FI_TRY(forward(f));
+    FI_TRY(backward(f));
+    FI_TRY(optimize(f));
+    if (out) FI_HIP_CHECK(hipEventRecord(f->e1, f->stream));
+    if (values) FI_HIP_CHECK(hipMemcpyAsync(values, f->val, (size_t)f->B * 4, hipMemcpyDeviceToHost, f->stream));
+    if (out) {
+        double l = 0.0;
+        FI_HIP_CHECK(hipMemcpyAsync(&l, f->loss, sizeof(double), hipMemcpyDeviceToHost, f->stream));
+        FI_HIP_CHECK(hipStreamSynchronize(f->stream));
+        float ms = 0.f;
+        FI_HIP_CHECK(hipEventElapsedTime(&ms, f->e0, f->e1));
+        out->loss = l;
+        out->step_ms = ms;
+        out->step = f->step;
+    } else if (values) {
+        FI_HIP_CHECK(hipStreamSynchronize(f->stream));
+    }
+    return FI_OK;
+}
+
+extern "C" int fi_farmer_forward(fi_farmer* f, const float* z, const float* x, int inputs_on_device, float* values) {
+    FI_REQUIRE(f && z && x && values, "farmer_forward: null argument");
+    FI_HIP_CHECK(hipSetDevice(f->dev));
+    FI_TRY(stage_inputs(f, z, x, nullptr, inputs_on_device));
+    FI_TRY(forward(f));
+    return d2h(f, f->val, values, (size_t)f->B);
+}
+
+extern "C" int fi_farmer_tensor(fi_farmer* f, const char* name, void** ptr, size_t* bytes) {
+    FI_REQUIRE(f && name && ptr && bytes, "farmer_tensor: null argument");
+    const size_t B = f->B, BT = (size_t)f->B * f->T;
+    struct E {
+        const char* n;
+        void* p;
+        size_t b;
+    } t[] = {{"params", f->params, f->off.total * 4}, {"grads", f->grads, f->off.total * 4},
+             {"values", f->val, B * 4},               {"z", f->z, BT * IN * 4},
+             {"x", f->x, B * XD * 4},                 {"targets", f->y, B * 4},
+             {"gates", f->gates, BT * G * 4},         {"h_last", f->cat, B * CAT * 4}};
+    for (const E& e : t)
+        if (std::strcmp(e.n, name) == 0) {
+            *ptr = e.p;
+            *bytes = e.b;
+            return FI_OK;
+        }
+    return fail(FI_ERR_INVALID, std::string("farmer_tensor: unknown tensor ") + name);
+}
+
+extern "C" void* fi_farmer_stream(fi_farmer* f) { return f ? (void*)f->stream : nullptr; }

@@ -26,6 +26,13 @@ int fail(int code, const std::string& msg);
         if (!(cond)) return ::fi::fail(FI_ERR_INVALID, (msg));       \
     } while (0)
 
+// propagate a non-OK status code
+#define FI_TRY(x)                     \
+    do {                              \
+        int _rc = (x);                \
+        if (_rc != FI_OK) return _rc; \
+    } while (0)
+
 constexpr int kWave = 64;
 
 // ------------------------------------------------------------------------------------

@@ -344,4 +344,30 @@ int f32_heads_wgrad_partial(const float* X, int I, const HeadsGrad& g, int split
     return launch(la, lb, EpiSlab{slab, N, (size_t)I * N}, I, N, g.rows, splits, s, cs_slab);
 }
 
+// ---- PyTorch-layout weights (W[N][K], nn.Linear): the FarmerLstm torso (farmer.hip)
+// Y[M][N] = X[M][K] W[N][K]^T + b (ReLU); ldx = row stride of X
+int f32_gemm_nt(const float* X, int ldx, int M, int K, const float* W, const float* bias, int N,
+                bool relu, float* Y, hipStream_t s) {
+    WMajor<GBM> la{X, ldx, M, K, ldx % 4 == 0 && K % 4 == 0 && aligned16(X)};
+    WMajor<GBN> lb{W, K, N, K, K % 4 == 0 && aligned16(W)};
+    return launch(la, lb, EpiBiasRelu{Y, N, bias, relu ? 1 : 0}, M, N, K, 1, s);
+}
+
+// dX[M][K] = dY[M][N] W[N][K], masked by (act > 0) when act != null (act: [M][K])
+int f32_gemm_nn_dgrad(const float* dY, int M, int N, const float* W, int K, const float* act, float* dX,
+                      hipStream_t s) {
+    WMajor<GBM> la{dY, N, M, N, N % 4 == 0 && aligned16(dY)};
+    KMajor<GBN> lb{W, K, N, K, K % 4 == 0 && aligned16(W)};
+    if (act) return launch(la, lb, EpiMask{dX, K, act}, M, K, N, 1, s);
+    return launch(la, lb, EpiBiasRelu{dX, K, nullptr, 0}, M, K, N, 1, s);
+}
+
+// weight-gradient partials in PyTorch layout: slab[split][N][K] = sum_{m in split} dY[m][N] X[m][K]
+int f32_gemm_tn_wgrad(const float* dY, int M, int N, const float* X, int ldx, int K, int splits, float* slab,
+                      hipStream_t s) {
+    KMajor<GBM> la{dY, N, M, N, N % 4 == 0 && aligned16(dY)};
+    KMajor<GBN> lb{X, ldx, M, K, ldx % 4 == 0 && K % 4 == 0 && aligned16(X)};
+    return launch(la, lb, EpiSlab{slab, K, (size_t)N * K}, N, K, M, splits, s);
+}
+
 }  // namespace fi

@@ -48,6 +48,13 @@ int f32_heads_wgrad_partial(const float* X, int I, const HeadsGrad& g, int split
 // misc.hip
 int colsum_partial(const float* Y, int M, int N, int splits, float* slab, hipStream_t s);
 int heads_colsum_partial(const HeadsGrad& g, int splits, float* slab, hipStream_t s);
+// PyTorch-layout (W[N][K]) fp32 GEMMs on the same MFMA kernel (farmer.hip)
+int f32_gemm_nt(const float* X, int ldx, int M, int K, const float* W, const float* bias, int N,
+                bool relu, float* Y, hipStream_t s);
+int f32_gemm_nn_dgrad(const float* dY, int M, int N, const float* W, int K, const float* act, float* dX,
+                      hipStream_t s);
+int f32_gemm_tn_wgrad(const float* dY, int M, int N, const float* X, int ldx, int K, int splits, float* slab,
+                      hipStream_t s);
 int reduce_slabs(float* slab, int splits, size_t count, float* out, hipStream_t s);  // slab is scratch (overwritten)
 // squared L2 norm of g -> *out; optionally also sums vt_nblk V-trace loss partials [i][3]
 // into vt_losses[0..2] in the same (final) launch

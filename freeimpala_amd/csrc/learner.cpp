@@ -132,12 +132,6 @@ static int dalloc(fi_learner* l, void** p, size_t bytes) {
     return FI_OK;
 }
 
-#define FI_TRY(x)                 \
-    do {                          \
-        int _rc = (x);            \
-        if (_rc != FI_OK) return _rc; \
-    } while (0)
-
 template <typename T>
 static int dalloc_n(fi_learner* l, T** p, size_t n) {
     return dalloc(l, (void**)p, n * sizeof(T));

@@ -6,8 +6,8 @@ import re
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def header_functions():
-    src = open(os.path.join(ROOT, "include", "fi_learner.h")).read()
+def header_functions(name="fi_learner.h"):
+    src = open(os.path.join(ROOT, "include", name)).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(fi_[a-z0-9_]+)\s*\(", src)))
 
@@ -21,6 +21,37 @@ def test_library_exports_every_header_symbol():
     assert not missing, missing
     assert set(names) == set(_abi.SIGNATURES), set(names) ^ set(_abi.SIGNATURES)
     assert lib.fi_abi_version() == 1
+
+
+def test_library_exports_every_farmer_header_symbol():
+    """include/fi_farmer.h (the FarmerLstm train step) is exported by the same library."""
+    from freeimpala_amd import farmer
+    lib = farmer.lib()
+    names = header_functions("fi_farmer.h")
+    assert len(names) >= 10
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    assert set(names) == set(farmer.SIGNATURES), set(names) ^ set(farmer.SIGNATURES)
+    assert farmer.param_count() == 1_514_497  # the reference model's size (SURVEY.md section 6)
+
+
+def test_farmer_struct_layouts_match_c():
+    import ctypes
+    import subprocess
+    import tempfile
+    from freeimpala_amd import farmer
+    src = ('#include <stdio.h>\n#include <stddef.h>\n#include "fi_farmer.h"\nint main(){printf("%zu %zu %zu %zu",'
+           'sizeof(fi_farmer_config), sizeof(fi_farmer_stats), offsetof(fi_farmer_config, device),'
+           'offsetof(fi_farmer_stats, step));}')
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "s.c")
+        open(c, "w").write(src)
+        subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", os.path.join(d, "s")], check=True)
+        out = subprocess.run([os.path.join(d, "s")], capture_output=True, text=True, check=True).stdout
+    got = [int(v) for v in out.split()]
+    exp = [ctypes.sizeof(farmer.FarmerConfig), ctypes.sizeof(farmer.FarmerStats),
+           farmer.FarmerConfig.device.offset, farmer.FarmerStats.step.offset]
+    assert got == exp
 
 
 def test_struct_layouts_match_c():
