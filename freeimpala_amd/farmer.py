@@ -178,6 +178,8 @@ class FarmerLstmModel:
         st = FarmerStats()
         _abi.check(lib().fi_farmer_train_step(self._h, zp, xp, tp, 1, None, C.byref(st) if stats else None),
                    "fi_farmer_train_step")
+        if stats:
+            self.last_step_ms = st.step_ms
         return st.loss if stats else None
 
     def upload_inputs(self, z, x, targets) -> None:
