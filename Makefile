@@ -38,10 +38,22 @@ build/host_learner_check: tests/cpp/host_learner_check.cpp include/freeimpala_am
 	g++ -std=c++17 -O2 -Wall -Iinclude $< -o $@ -L$(LIBDIR) -lfi_learner -pthread '-Wl,-rpath,$$ORIGIN/../$(LIBDIR)' -Wl,-rpath,/opt/rocm/lib
 
 # the cmd/freeimpala-shaped binary on freeimpala_amd::Learner (include/freeimpala_amd/learner.hpp)
-tools: build/fi_freeimpala
-build/fi_freeimpala: tools/fi_freeimpala.cpp $(wildcard include/freeimpala_amd/*.hpp) include/fi_learner.h $(LIBDIR)/libfi_learner.so
+tools: build/fi_freeimpala build/fi_freeimpala_mpi
+build/fi_freeimpala: tools/fi_freeimpala.cpp tools/cli_common.hpp $(wildcard include/freeimpala_amd/*.hpp) include/fi_learner.h $(LIBDIR)/libfi_learner.so
 	@mkdir -p build
 	g++ -std=c++17 -O2 -Wall -Wextra -Iinclude $< -o $@ -L$(LIBDIR) -lfi_learner -pthread '-Wl,-rpath,$$ORIGIN/../$(LIBDIR)' -Wl,-rpath,/opt/rocm/lib
+
+# the freeimpala_mpi_async_pool-shaped binary (MPICH from /opt/conda; system libstdc++ first in
+# the RPATH so conda's older copy is not picked up)
+MPI_HOME ?= /opt/conda
+MPI_LINK := $(MPI_HOME)/lib/libmpi.so -Wl,--disable-new-dtags -Wl,-rpath,/usr/lib/x86_64-linux-gnu:$(MPI_HOME)/lib
+build/fi_freeimpala_mpi: tools/fi_freeimpala_mpi.cpp tools/cli_common.hpp $(wildcard include/freeimpala_amd/*.hpp) include/fi_learner.h $(LIBDIR)/libfi_learner.so
+	@mkdir -p build
+	g++ -std=c++17 -O2 -Wall -Wextra -Iinclude -I$(MPI_HOME)/include $< -o $@ -L$(LIBDIR) -lfi_learner -pthread '-Wl,-rpath,$$ORIGIN/../$(LIBDIR)' -Wl,-rpath,/opt/rocm/lib $(MPI_LINK)
+build/mpi_pool_check: tests/cpp/mpi_pool_check.cpp $(wildcard include/freeimpala_amd/*.hpp)
+	@mkdir -p build
+	g++ -std=c++17 -O2 -Wall -Wextra -Iinclude -I$(MPI_HOME)/include $< -o $@ -pthread $(MPI_LINK)
+host: build/mpi_pool_check
 
 clean:
 	rm -rf build $(LIBDIR)
