@@ -121,6 +121,18 @@ constexpr int IMG = 2 * PLANE;                      // 56,576 B
 constexpr int OUT = 400 * 32 * 2;                   // 25,600 B output / dY tile
 }  // namespace c1
 
+// sum of a fragment's 8 bf16 values into acc: 4 v_dot2c_f32_bf16 against (1, 1) instead of 8
+// conversions + 8 adds (the weight-gradient waves' bias column sums of dY)
+__device__ __forceinline__ float sum8_bf16(const bf16x8& v, float acc) {
+    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+    struct P4 { bf16x2 p[4]; };
+    const P4 pv = __builtin_bit_cast(P4, v);
+    const bf16x2 one = {(__bf16)1.0f, (__bf16)1.0f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_fdot2_f32_bf16(pv.p[j], one, acc, false);
+    return acc;
+}
+
 __device__ __forceinline__ void u8x16_to_bf16(u32x4 v, bf16x8& lo, bf16x8& hi) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -1151,11 +1163,8 @@ __global__ __launch_bounds__(512, 2) void conv2_bwd_fr(const __bf16* __restrict_
             for (int ms = 0; ms < 6; ++ms) {
                 const bf16x8* cur = fb[ms & 1];
                 if (ms + 1 < 6) load(ms + 1, fb[(ms + 1) & 1]);
-                float s0 = 0.f, s1 = 0.f;  // bias: column sums of dY (kept by wave 0)
-#pragma unroll
-                for (int j = 0; j < 8; ++j) { s0 += (float)cur[0][j]; s1 += (float)cur[1][j]; }
-                bsum0 += s0;
-                bsum1 += s1;
+                bsum0 = sum8_bf16(cur[0], bsum0);  // bias: column sums of dY (kept by wave 0)
+                bsum1 = sum8_bf16(cur[1], bsum1);
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
                     accw[t][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[2 + t], cur[0], accw[t][0], 0, 0, 0);
@@ -1326,6 +1335,12 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
     const int lane = threadIdx.x & 63, tid = threadIdx.x;
     const int w = wave_id(), wr = w & 3;
     const int g = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3, h = lane >> 5, col = lane & 31;
+    // waves 4-7 carry the critical path (conv2's data gradient, then conv1's weight gradient;
+    // per-phase clocks: 6.3k + 2.7k per frame against waves 0-3's 1.5k + 1.8k + 3.8k parked at
+    // the barriers): at s_setprio 1 their MFMAs and VALU win the SIMD's arbitration and waves
+    // 0-3 fill the gaps (MI355X_MICROARCH.md, two waves per SIMD, item 4): 8.32 -> 7.89 ms.
+    // The same for conv12_fwd / conv3_bwd (either half) measured time-neutral.
+    if (w >= 4) __builtin_amdgcn_s_setprio(1);
     const uint32_t lds0 = lds_addr(smem);
     uint32_t* tab = (uint32_t*)(smem + c21::O_TAB);
     // a1 planar (conv12_fwd_fr wrote it in this image's order): the a1 pieces are linear 1-KiB
@@ -1475,11 +1490,8 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                 for (int ms = 0; ms < 6; ++ms) {
                     const bf16x8* cur = fb[ms & 1];
                     if (ms + 1 < 6) load(ms + 1, fb[(ms + 1) & 1]);
-                    float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) { s0 += (float)cur[0][j]; s1 += (float)cur[1][j]; }
-                    bsum0 += s0;
-                    bsum1_ += s1;
+                    bsum0 = sum8_bf16(cur[0], bsum0);
+                    bsum1_ = sum8_bf16(cur[1], bsum1_);
 #pragma unroll
                     for (int t = 0; t < 4; ++t) {
                         accw[t][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[2 + t], cur[0], accw[t][0], 0, 0, 0);
@@ -1933,11 +1945,8 @@ __device__ __forceinline__ void c3_wgrad(const C3Ctx& ctx, char* smem, float* sl
         for (int ms = 0; ms < 4; ++ms) {
             const bf16x8* cur = fb[ms & 1];
             if (ms + 1 < 4) load(ms + 1, fb[(ms + 1) & 1]);
-            float s0 = 0.f, s1 = 0.f;  // bias: column sums of dY (kept by wave 0)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) { s0 += (float)cur[0][j]; s1 += (float)cur[1][j]; }
-            bsum0 += s0;
-            bsum1 += s1;
+            bsum0 = sum8_bf16(cur[0], bsum0);  // bias: column sums of dY (kept by wave 0)
+            bsum1 = sum8_bf16(cur[1], bsum1);
 #pragma unroll
             for (int i = 0; i < NKT; ++i) {
                 accw[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[2 + i], cur[0], accw[i][0], 0, 0, 0);

@@ -3,7 +3,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 for L in ${LIBS:-ph}; do
-  FI_LIB_OVERRIDE=build/exp/lib_$L.so timeout -k 10 200 python bench.py --steps 3 --warmup 2 --profile-steps 1 --no-cpu-baseline > gpurun_out/ph_$L.json 2> gpurun_out/ph_$L.txt || exit 1
+  FI_LIB_OVERRIDE=build/ab/lib_$L.so timeout -k 10 200 python bench.py --steps 3 --warmup 2 --profile-steps 1 --no-cpu-baseline > gpurun_out/ph_$L.json 2> gpurun_out/ph_$L.txt || exit 1
   echo "== $L $(python3 -c "import json; d=json.load(open('gpurun_out/ph_$L.json')); k=d['kernel_ms_per_step']; print(d['ms_per_step'], {x: k[x] for x in list(k)[:3]})")"
   grep "phases ${PH_KERNEL:-conv21}" gpurun_out/ph_$L.txt
 done
