@@ -268,7 +268,7 @@ public:
         return true;
     }
 
-    // mpi_async_pool/main.cpp:451-454
+    // mpi_async_pool/main.cpp:457-460
     void terminate() { MPI_Send(nullptr, 0, MPI_CHAR, dst_, TAG_TERMINATE, comm_); }
 
 private:
