@@ -22,11 +22,13 @@
 #pragma once
 
 #include <cstdint>
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "fi_learner.h"
@@ -49,6 +51,8 @@ struct LearnerConfig {
     float gamma = 0.99f;       // --gamma (synthetic generator only)
     fi_vtrace_hparams hp{1.f, 1.f, 1.f, 1.f, 0.5f, 0.01f};
     std::vector<int> devices{0};     // --devices 0,1,... (player p -> devices[p % n])
+    size_t data_parallel = 1;  // --data-parallel G: each player's batch split over G devices
+                               // (shard g of player p on devices[(p G + g) % n]; RCCL all-reduce)
     uint64_t seed = 42;        // --seed (parameter init)
 
     size_t entry_records() const { return entry_size ? entry_size : seq_length + 1; }
@@ -84,6 +88,7 @@ struct LearnerConfig {
             else if (f == "--max-grad-norm") c.max_grad_norm = (float)num(f, v);
             else if (f == "--gamma") c.gamma = (float)num(f, v);
             else if (f == "--seed") c.seed = (uint64_t)num(f, v);
+            else if (f == "--data-parallel") c.data_parallel = (size_t)num(f, v);
             else if (f == "--devices") {
                 c.devices.clear();
                 std::string s = v;
@@ -106,6 +111,8 @@ struct LearnerConfig {
         if (c.arch != "mlp" && c.arch != "atari") throw std::invalid_argument("--learner-arch: mlp|atari");
         if (c.optimizer != "adam" && c.optimizer != "sgd") throw std::invalid_argument("--optimizer: adam|sgd");
         if (c.publish != "fp32" && c.publish != "bf16") throw std::invalid_argument("--publish: fp32|bf16");
+        if (c.data_parallel == 0 || c.batch_size % c.data_parallel != 0)
+            throw std::invalid_argument("--data-parallel must divide --batch-size");
         return c;
     }
 
@@ -136,6 +143,7 @@ struct LearnerConfig {
         c.max_grad_norm = (float)num("--max-grad-norm", str("--max-grad-norm"));
         c.gamma = (float)num("--gamma", str("--gamma"));
         c.seed = (uint64_t)num("--learner-seed", str("--learner-seed"));
+        c.data_parallel = (size_t)num("--data-parallel", str("--data-parallel"));
         const char* argv[] = {"", "--devices", nullptr};
         const std::string dev = str("--devices");
         argv[2] = dev.c_str();
@@ -147,19 +155,20 @@ struct LearnerConfig {
         return c;
     }
 
-    // The C-ABI configuration of player p's handle.
-    fi_learner_config abi_config(size_t p) const {
+    // The C-ABI configuration of player p's handle (shard g of it under --data-parallel: the
+    // same seed, so every replica starts from the same parameters).
+    fi_learner_config abi_config(size_t p, size_t g = 0) const {
         fi_learner_config k;
         fi_learner_config_init(&k);
         k.arch = arch == "atari" ? FI_ARCH_ATARI : FI_ARCH_MLP;
         k.seq_len = (int32_t)seq_length;
-        k.batch = (int32_t)batch_size;
+        k.batch = (int32_t)(batch_size / data_parallel);
         k.num_actions = num_actions;
         k.obs_dim = obs_dim;
         k.hidden = hidden;
         k.optimizer = optimizer == "sgd" ? FI_OPT_SGD : FI_OPT_ADAM;
         k.publish_dtype = publish == "bf16" ? FI_PUBLISH_BF16 : FI_PUBLISH_FP32;
-        k.device = devices[p % devices.size()];
+        k.device = devices[(p * data_parallel + g) % devices.size()];
         k.gamma = gamma;
         k.hp = hp;
         k.lr = lr;
@@ -191,6 +200,8 @@ void add_learner_arguments(Parser& program) {
     program.add_argument("--learner-seed").help("Parameter-initialisation seed").default_value(std::to_string(d.seed));
     program.add_argument("--devices").help("HIP devices, comma separated (player p -> devices[p % n])")
         .default_value(std::string("0"));
+    program.add_argument("--data-parallel").help("Devices per player: the batch is split over them, RCCL all-reduce")
+        .default_value(std::string("1"));
 }
 
 class DeviceLearner {
@@ -198,12 +209,24 @@ public:
     explicit DeviceLearner(const LearnerConfig& cfg) : cfg_(cfg), stats_(cfg.players), err_(cfg.players) {
         if (fi_abi_version() != FI_ABI_VERSION)
             throw std::runtime_error("libfi_learner ABI version mismatch");
+        const size_t G = cfg.data_parallel ? cfg.data_parallel : 1;
         handles_.resize(cfg.players, nullptr);
+        shards_.assign(cfg.players, std::vector<fi_learner*>(G, nullptr));
         for (size_t p = 0; p < cfg.players; ++p) {
-            const fi_learner_config k = cfg.abi_config(p);
-            if (fi_learner_create(&k, &handles_[p]) != FI_OK) {
-                const std::string msg = std::string("fi_learner_create(player ") + std::to_string(p) +
-                                        "): " + fi_last_error();
+            for (size_t g = 0; g < G; ++g) {
+                const fi_learner_config k = cfg.abi_config(p, g);
+                if (fi_learner_create(&k, &shards_[p][g]) != FI_OK) {
+                    const std::string msg = std::string("fi_learner_create(player ") + std::to_string(p) +
+                                            ", shard " + std::to_string(g) + "): " + fi_last_error();
+                    release();
+                    throw std::runtime_error(msg);
+                }
+            }
+            handles_[p] = shards_[p][0];
+            // one RCCL communicator per player over its G devices: the in-step all-reduce sums
+            // the shards' gradients, every replica applies the same update
+            if (G > 1 && fi_comm_init_all(shards_[p].data(), (int)G) != FI_OK) {
+                const std::string msg = std::string("fi_comm_init_all(player ") + std::to_string(p) + "): " + fi_last_error();
                 release();
                 throw std::runtime_error(msg);
             }
@@ -223,6 +246,7 @@ public:
             if (batch[i].size() != eb) return fail(player_index, "entries of different sizes");
             ptrs[i] = batch[i].data();
         }
+        if (shards_[player_index].size() > 1) return step_sharded(player_index, ptrs, eb);
         fi_step_stats st{};
         if (fi_learner_step(handles_[player_index], ptrs.data(), ptrs.size(), eb, &st) != FI_OK)
             return fail(player_index, fi_last_error());
@@ -234,6 +258,7 @@ public:
     // drop it and block in readBatch for the next one); wait() completes it.
     bool step_async(size_t player_index, const std::vector<std::vector<char>>& batch) {
         if (player_index >= handles_.size()) return fail(0, "player_index out of range");
+        if (shards_[player_index].size() > 1) return fail(player_index, "step_async: not with --data-parallel > 1");
         if (batch.empty()) return fail(player_index, "empty batch");
         const size_t eb = batch[0].size();
         std::vector<const void*> ptrs(batch.size());
@@ -252,6 +277,7 @@ public:
     template <class Fill>
     bool step_staged(size_t player_index, Fill&& fill, bool async = false) {
         if (player_index >= handles_.size()) return fail(0, "player_index out of range");
+        if (shards_[player_index].size() > 1) return fail(player_index, "step_staged: not with --data-parallel > 1");
         fi_learner* h = handles_[player_index];
         void* dst = nullptr;
         size_t stride = 0;
@@ -284,7 +310,8 @@ public:
     }
     bool load_state(size_t p, const std::vector<char>& blob) {
         if (p >= handles_.size()) return fail(0, "player_index out of range");
-        if (fi_learner_load_state(handles_[p], blob.data(), blob.size()) != FI_OK) return fail(p, fi_last_error());
+        for (fi_learner* h : shards_[p])
+            if (fi_learner_load_state(h, blob.data(), blob.size()) != FI_OK) return fail(p, fi_last_error());
         return true;
     }
 
@@ -300,8 +327,8 @@ public:
     // --starting-model resume (Model::loadFromDisk bytes + version).
     bool load(size_t p, const std::vector<char>& blob, uint64_t version) {
         if (p >= handles_.size()) return fail(0, "player_index out of range");
-        if (fi_learner_set_params(handles_[p], blob.data(), blob.size(), version) != FI_OK)
-            return fail(p, fi_last_error());
+        for (fi_learner* h : shards_[p])
+            if (fi_learner_set_params(h, blob.data(), blob.size(), version) != FI_OK) return fail(p, fi_last_error());
         return true;
     }
 
@@ -314,23 +341,58 @@ public:
         return err_.at(p);
     }
     fi_learner* handle(size_t p) { return handles_.at(p); }
+    size_t shards(size_t p = 0) const { return shards_.at(p).size(); }
     const LearnerConfig& config() const { return cfg_; }
 
 private:
+    // --data-parallel: contiguous shards of the M entries, one per device, stepped
+    // concurrently (the in-step all-reduce needs every rank); loss sums added over the shards
+    bool step_sharded(size_t p, const std::vector<const void*>& ptrs, size_t eb) {
+        const size_t G = shards_[p].size();
+        if (ptrs.size() % G != 0) return fail(p, "batch not divisible by --data-parallel");
+        const size_t per = ptrs.size() / G;
+        std::vector<fi_step_stats> st(G);
+        std::vector<int> rc(G, FI_OK);
+        std::vector<std::string> why(G);
+        auto run = [&](size_t g) {
+            rc[g] = fi_learner_step(shards_[p][g], ptrs.data() + g * per, per, eb, &st[g]);
+            if (rc[g] != FI_OK) why[g] = fi_last_error();  // thread-local: read on the same thread
+        };
+        std::vector<std::thread> th;
+        for (size_t g = 1; g < G; ++g) th.emplace_back(run, g);
+        run(0);
+        for (auto& t : th) t.join();
+        for (size_t g = 0; g < G; ++g)
+            if (rc[g] != FI_OK) return fail(p, "shard " + std::to_string(g) + ": " + why[g]);
+        fi_step_stats sum = st[0];
+        for (size_t g = 1; g < G; ++g) {
+            sum.pg_loss += st[g].pg_loss;
+            sum.baseline_loss += st[g].baseline_loss;
+            sum.entropy_loss += st[g].entropy_loss;
+            sum.total_loss += st[g].total_loss;
+            sum.step_ms = std::max(sum.step_ms, st[g].step_ms);
+        }
+        stats_[p] = sum;
+        return true;
+    }
+
     bool fail(size_t p, const std::string& m) {
         std::lock_guard<std::mutex> g(mu_);
         err_.at(p < err_.size() ? p : 0) = m;
         return false;
     }
     void release() {
-        for (auto& h : handles_) {
-            if (h) fi_learner_destroy(h);
-            h = nullptr;
-        }
+        for (auto& v : shards_)
+            for (auto& h : v) {
+                if (h) fi_learner_destroy(h);
+                h = nullptr;
+            }
+        for (auto& h : handles_) h = nullptr;
     }
 
     LearnerConfig cfg_;
-    std::vector<fi_learner*> handles_;
+    std::vector<fi_learner*> handles_;               // per player: shard 0 (publishes, checkpoints)
+    std::vector<std::vector<fi_learner*>> shards_;  // per player: its G data-parallel replicas
     std::vector<fi_step_stats> stats_;
     mutable std::mutex mu_;
     std::vector<std::string> err_;

@@ -182,7 +182,13 @@ private:
         while (!should_stop_.load() && iteration_count < total_iterations_) {
             bool got = false;
             if constexpr (detail::has_read_batch_into<Buffer>::value) {
-                got = step_zero_copy(player_index);
+                if (device_->shards(player_index) == 1) {
+                    got = step_zero_copy(player_index);
+                } else {  // --data-parallel: readBatch, then the shards step concurrently
+                    auto batch = shared_buffers_[player_index]->readBatch(batch_size_);
+                    got = !batch.empty();
+                    if (got) step(player_index, batch);
+                }
             } else {
                 auto batch = shared_buffers_[player_index]->readBatch(batch_size_);
                 got = !batch.empty();

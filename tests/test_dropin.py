@@ -55,7 +55,7 @@ def test_cli_parses_reference_command_line_strictly():
     assert r.returncode == 0
     for flag in ("--players", "--iterations", "--buffer-capacity", "--batch-size", "--entry-size",
                  "--agents", "--game-steps", "--learner-time", "--checkpoint-freq", "--seq-length",
-                 "--learner-arch", "--lr", "--devices", "--optimizer", "--publish"):
+                 "--learner-arch", "--lr", "--devices", "--optimizer", "--publish", "--data-parallel"):
         assert flag in r.stdout, flag
     assert run(["--no-such-flag", "3"]).returncode == 1
     assert run(["--players", "two"]).returncode == 1
@@ -63,6 +63,8 @@ def test_cli_parses_reference_command_line_strictly():
     # main.cpp:164-176 validation
     assert run(CONFIG1[:6] + ["--batch-size", "64"]).returncode == 1
     assert run(["--entry-size", "10", "--game-steps", "20"]).returncode == 1
+    # --data-parallel G splits each player's M entries over G devices: G must divide M
+    assert run(CONFIG1 + ["--data-parallel", "3"]).returncode == 1
 
 
 def test_cli_without_gpu_fails_loudly():
