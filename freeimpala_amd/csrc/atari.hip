@@ -731,7 +731,7 @@ struct AtariImpl {
     bool a1_planar = true; // fused fwd + bwd: a1 stored in conv21's image order (FI_A1_NHWC=1 -> NHWC)
     int fr_grid = 256;     // persistent frame-resident workgroups, 1 per CU (FI_FR_GRID=g: tests put
                            // many frames on each workgroup at small N to reach the steady state)
-    FcBlasLt* fc = nullptr;  // fc layer GEMMs (hipBLASLt)
+    FcBlasLt* fc = nullptr;  // fc forward / dgrad on hipBLASLt (null with FI_FC_OWN=1: fc_gemm.hip)
 };
 
 int conv1_fwd_fr_launch(const uint8_t* frames, const __bf16* w1t, const float* bias, __bf16* a1,
@@ -766,7 +766,7 @@ static bool dmalloc(AtariImpl* I, T** p, size_t n) {
 }
 
 // split factors (blocks over the reduction) per weight-gradient GEMM
-constexpr int SPL_H = 128, SPL_FC = 8, SPL_C3 = 160, SPL_C2 = 256, SPL_C1 = 512;
+constexpr int SPL_H = 128, SPL_FC = 9, SPL_C3 = 160, SPL_C2 = 256, SPL_C1 = 512;
 constexpr int GBM = 128;  // M-tile of the dgrad GEMMs (class stride granularity)
 
 AtariNet* atari_create(int B, int T, int A) {
@@ -814,12 +814,15 @@ AtariNet* atari_create(int B, int T, int A) {
         atari_destroy(n);
         return nullptr;
     }
-    I->fc = fc_blaslt_create((int)N, I->a3, I->wb.fcB, I->dh, I->h, I->da3, I->slab, s0);
-    (void)hipStreamDestroy(s0);
-    if (!I->fc) {  // fc_blaslt_create set the error
-        atari_destroy(n);
-        return nullptr;
+    if (!std::getenv("FI_FC_OWN")) {
+        I->fc = fc_blaslt_create((int)N, I->a3, I->wb.fcB, I->dh, I->h, I->da3, s0);
+        if (!I->fc) {  // fc_blaslt_create set the error
+            (void)hipStreamDestroy(s0);
+            atari_destroy(n);
+            return nullptr;
+        }
     }
+    (void)hipStreamDestroy(s0);
     return n;
 }
 
@@ -875,7 +878,11 @@ int atari_forward(AtariNet* n, const uint8_t* frames, float* logits, float* valu
     } else { TagScope ts(tg, "conv3_fwd"); rc = gemm<128, 64, 2, 2>(ConvGather<9, 64, 3, 1, 7>{I->a2, N * P3}, RowsBf16{I->wb.c3T, C3O, C3K},
                              EpiAct{I->a3, C3O, p + o.c3b, 1.0f}, N * P3, C3O, C3K, s); }
     if (rc) return rc;
-    { TagScope ts(tg, "fc_fwd"); rc = fc_blaslt_forward(I->fc, I->a3, I->wb.fcB, p + o.fcb, I->h, s); }
+    {
+        TagScope ts(tg, "fc_fwd");
+        rc = I->fc ? fc_blaslt_forward(I->fc, I->a3, I->wb.fcB, p + o.fcb, I->h, s)
+                   : fc_fwd_launch(I->a3, I->wb.fcT, p + o.fcb, I->h, N, s);
+    }
     if (rc) return rc;
     { TagScope ts(tg, "heads_fwd"); rc = gemm<128, 32, 4, 1>(RowsBf16{I->h, N, FCO}, RowsBf16{I->wb.hT, HP, FCO},
                              EpiHeadsOut{logits, values, p + o.hb, I->A}, N, HP, FCO, s); }
@@ -911,13 +918,15 @@ int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, con
         FI_A("reduce_slabs", reduce_slabs(slab, kColsumSplits, (size_t)FCO, grads + o.fcb, s));
     }
     // fc: wgrad [3136][512] + bias, dgrad -> da3 (masked by a3)
-    // fc (hipBLASLt): wgrad straight into the gradient blob, bias = column sums of dh,
-    // dgrad -> da3 unmasked (conv3's backward applies the a3 ReLU mask as it loads da3)
-    FI_A("fc_wgrad", fc_blaslt_wgrad(I->fc, I->a3, I->dh, grads + o.fcw, s));
+    // fc: wgrad (fc_gemm.hip) as fp32 slabs reduced into the gradient blob, bias = column
+    // sums of dh (left by heads dgrad), dgrad -> da3 unmasked (conv3's backward applies the
+    // a3 ReLU mask as it loads da3)
+    FI_A("fc_wgrad", fc_wgrad_launch(I->a3, I->dh, slab, grads + o.fcw, N, s));
     // buckets in reverse layer order: fc + heads (95 % of the gradient bytes) reduce while
     // fc dgrad, conv3 and conv2/conv1 backward run
     if (gr && (rc = gr->ready(o.fcw, o.total - o.fcw))) return rc;
-    FI_A("fc_dgrad", fc_blaslt_dgrad(I->fc, I->dh, I->wb.fcB, I->da3, s));
+    FI_A("fc_dgrad", I->fc ? fc_blaslt_dgrad(I->fc, I->dh, I->wb.fcB, I->da3, s)
+                           : fc_dgrad_launch(I->dh, I->wb.fcB, I->da3, N, s));
     // conv3: wgrad [576][64] + bias, dgrad -> da2 (masked by a2)
     if (I->fr) {
         const int grid = std::min(N, I->fr_grid);

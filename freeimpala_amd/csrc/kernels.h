@@ -55,6 +55,11 @@ int f32_gemm_nn_dgrad(const float* dY, int M, int N, const float* W, int K, cons
                       hipStream_t s);
 int f32_gemm_tn_wgrad(const float* dY, int M, int N, const float* X, int ldx, int K, int splits, float* slab,
                       hipStream_t s);
+// fc_gemm.hip (the Atari fc layer, 3136 -> 512, rows = (T+1)*B)
+int fc_fwd_launch(const __bf16* a3, const __bf16* wT, const float* bias, __bf16* h, int rows, hipStream_t s);
+int fc_dgrad_launch(const __bf16* dh, const __bf16* w, __bf16* da3, int rows, hipStream_t s);  // da3 unmasked
+int fc_wgrad_splits(int rows);  // R-slices (fp32 slabs of 3136 x 512) fc_wgrad_launch uses
+int fc_wgrad_launch(const __bf16* a3, const __bf16* dh, float* slab, float* dw, int rows, hipStream_t s);
 int reduce_slabs(float* slab, int splits, size_t count, float* out, hipStream_t s);  // slab is scratch (overwritten)
 // squared L2 norm of g -> *out; optionally also sums vt_nblk V-trace loss partials [i][3]
 // into vt_losses[0..2] in the same (final) launch

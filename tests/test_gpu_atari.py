@@ -83,8 +83,8 @@ def _check_step_against_oracle(orc, L, T, B, A, a1_planar=False, da1=None):
     dout[:T * B, :A] = dl.reshape(T * B, A)
     dout[:, A] = dv.reshape(N)
     g_ref, mids = orc.atari_backward_ex(frames, p0, gpu_acts, dout, A=A, bf16_emul=True)
-    # da3 is stored before its ReLU mask (the fc dgrad is a plain library GEMM; conv3's
-    # backward applies (a3 > 0) as it loads da3), so mask it here
+    # da3 is stored before its ReLU mask (conv3's backward applies (a3 > 0) as it loads da3),
+    # so mask it here
     dev = {nm: bf16_to_f32(L.tensor(nm, np.uint16, sh)) for nm, sh in
            [("dh", (N, 512)), ("da3", (N, 7, 7, 64)), ("da2", (N, 9, 9, 64))]}
     dev["da1"] = bf16_to_f32(L.tensor("da1", np.uint16, (N, 20, 20, 32))) if da1 is None else da1
@@ -276,26 +276,30 @@ def test_fused_conv21_backward_without_da1_store(monkeypatch):
     np.testing.assert_array_equal(gs[0], gs[1])
 
 
-def test_fc_wgrad_split_matches_single_gemm(monkeypatch):
-    """fc weight gradient as a strided batch of row-block GEMMs + a fixed-order sum of the
-    partials (the faster form at the bench shape) against the single GEMM: fcW within fp32
-    summation-order rounding, every other gradient bit-identical. 16,384 frames, 8 blocks."""
-    T, B = 3, 4096
-    fcw = slice(77984, 77984 + 3136 * 512)
-    gs = {}
-    monkeypatch.setenv("FI_FC_SPLIT", "8")
-    for mode in ("0", "2"):
-        monkeypatch.setenv("FI_FC_WGRAD", mode)
-        L = mk(T=T, B=B, seed=6)
-        L.synth(seed=23)
-        L.step_resident()
-        gs[mode] = L.tensor("grads")
-        L.close()
-    a, b = gs["2"], gs["0"]
-    assert np.isfinite(a).all()
-    rel(a[fcw], b[fcw], "fcW", l2=1e-5, mx=1e-4)
-    np.testing.assert_array_equal(a[:fcw.start], b[:fcw.start])
-    np.testing.assert_array_equal(a[fcw.stop:], b[fcw.stop:])
+@pytest.mark.parametrize("T,B", [(3, 4096), (11, 1365)])  # 16,384 frames; 16,380 (ragged tiles)
+def test_fc_layer_kernels_vs_fp32_gemm(orc, T, B, monkeypatch):
+    """The hand-written fc kernels (fc_gemm.hip) at sizes where every persistent workgroup of
+    the forward / dgrad walks several output tiles (the staging pipeline running across tile
+    boundaries) and the weight gradient splits R into 9 slabs, against fp32 GEMMs of the GPU's
+    own bf16 inputs: h = relu(a3 . W + b) and da3 = dh . W^T to a bf16 rounding, dW = a3^T . dh
+    to fp32 summation-order rounding. R = 16,380 leaves a partial last row tile. FI_FC_OWN=1
+    puts the forward and data gradient on the hand-written kernels too."""
+    N = (T + 1) * B
+    monkeypatch.setenv("FI_FC_OWN", "1")
+    L = mk(T=T, B=B, seed=6)
+    L.synth(seed=23)
+    p0 = L.get_params()
+    L.step_resident()
+    f32 = lambda nm, sh: bf16_to_f32(L.tensor(nm, np.uint16, sh))
+    a3, h, dh, da3 = f32("a3", (N, 3136)), f32("h", (N, 512)), f32("dh", (N, 512)), f32("da3", (N, 3136))
+    fcw0, fcb0 = 77984, 77984 + 3136 * 512
+    W = orc.bf16_round(p0[fcw0:fcb0].reshape(3136, 512)).astype(np.float32)
+    h_ref = np.maximum(a3 @ W + p0[fcb0:fcb0 + 512], 0)
+    rel(h, h_ref, "h", l2=4e-3, mx=1e-2)
+    rel(da3, dh @ W.T, "da3", l2=4e-3, mx=1e-2)
+    g = L.tensor("grads")
+    rel(g[fcw0:fcb0], (a3.T @ dh).ravel(), "fcW", l2=1e-5, mx=1e-4)
+    L.close()
 
 
 def test_atari_full_size_sampled_forward_and_determinism(orc):
@@ -364,16 +368,19 @@ def test_a1_planar_layout_matches_nhwc(monkeypatch):
     np.testing.assert_array_equal(outs["planar"]["p"], outs["nhwc"]["p"])
 
 
-def test_deterministic_mode_is_bit_exact_across_processes(tmp_path):
-    """The fc GEMM algorithms are chosen by timing at creation (per process), so two runs can
-    round differently; FI_DETERMINISTIC=1 takes the heuristic's first solution and the direct
-    weight-gradient form instead: two separate processes then produce the same gradient blob
-    bit for bit."""
+@pytest.mark.parametrize("mode", ["FI_DETERMINISTIC", "FI_FC_OWN"])
+def test_deterministic_mode_is_bit_exact_across_processes(tmp_path, mode):
+    """hipBLASLt's fc forward / dgrad algorithms are chosen by timing at creation (per process),
+    so two runs can round differently; FI_DETERMINISTIC=1 takes the heuristic's first solution
+    instead. With FI_FC_OWN=1 every fc GEMM runs on the hand-written kernels (fixed tiles and
+    k order, fixed-order slab sums): deterministic by construction. Either way two separate
+    processes produce the same gradient blob bit for bit."""
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, FI_DETERMINISTIC="1")
+    env = dict(os.environ)
+    env[mode] = "1"
     outs = []
     for i in range(2):
         f = tmp_path / f"g{i}.npy"
