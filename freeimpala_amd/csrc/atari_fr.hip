@@ -1714,8 +1714,8 @@ int conv21_bwd_fr_launch(const __bf16* a1, const __bf16* da2, const __bf16* w2d,
 //     conv2 (sig) both 16-lane groups of a ds_read_b128 are conflict-free.
 //   The weight-gradient reduction walks s = 20..83 (dY zero where it is border), A pixel
 //     s - 20 + 9ky + kx: 4 consecutive s x chunk offsets {0, 8, 4, 12}.
-// a3 arrives through the same gather table as da3, so the wave that DMAs dY piece j also
-// DMAs mask piece j and applies the mask to its own piece before the frame barrier.
+// a3 (da3's ReLU mask) arrives beside da3 in the same byte order; the wave that DMAs and
+// reshuffles da3 piece j applies the mask of piece j on the way.
 // Waves 0-3: weight gradient (k-tiles kt = wr + 4i = (tap 2i + (wr>>1), channel half wr&1))
 // and all DMA issue; waves 4-7: data gradient, transposed on 16x16x32 (wave = channel half
 // wr&1 x pixel half wr>>1, W3 slice in registers), dX stored from registers.
@@ -1723,23 +1723,8 @@ int conv21_bwd_fr_launch(const __bf16* a1, const __bf16* da2, const __bf16* w2d,
 namespace c3 {
 constexpr int XB = 12 * 1024;                // 768 units (8 chunk planes of 96)
 constexpr int DYB = 16 * 1024;               // 1,009 used units -> 16 KiB
-constexpr int MB = 16 * 1024;                // a3 image, same layout as dY
-[[maybe_unused]] constexpr int SLOT = XB + DYB + MB;  // 45,056 (FI_C3_GATHER)
-[[maybe_unused]] constexpr int RING = 3;
-constexpr int NX = XB / 1024, NDY = DYB / 1024;  // 12 + 16 (+ 16 mask) pieces
-static_assert(NX == 12 && NDY == 16, "c3_issue assigns 3 X + 4 dY + 4 mask pieces per wave");
 __host__ __device__ constexpr int zc(int c) { return 8 * (c & 1) + 4 * ((c >> 1) & 1); }
 }  // namespace c3
-
-__device__ __forceinline__ uint32_t c3_x_src(int u) {  // X image unit -> a2 byte offset
-    const int c = u / 96, k = u - 96 * c - c3::zc(c);
-    return k >= 0 && k <= 80 ? (uint32_t)(k * 128 + 16 * c) : FI_OOB;
-}
-__device__ __forceinline__ uint32_t c3_dy_src(int v) {  // dY / mask image unit -> da3 / a3 byte offset
-    const int c = v >> 7, k = (v & 127) - c3::zc(c), Y = k / 9, X = k - 9 * Y;
-    const bool inside = k >= 0 && k <= 100 && Y >= 2 && Y <= 8 && X >= 2 && X <= 8;
-    return inside ? (uint32_t)(((Y - 2) * 7 + X - 2) * 128 + 16 * c) : FI_OOB;
-}
 
 struct C3Ctx {
     const __bf16 *a2, *da3, *a3;
@@ -1747,35 +1732,13 @@ struct C3Ctx {
     int nframes;
 };
 
-// wave w < 4 issues X pieces w, w+4, w+8 and dY / mask pieces w, w+4, w+8, w+12 of frame f
-__device__ __forceinline__ void c3_issue(const C3Ctx& c, const uint32_t* tab, int f, uint32_t slot_lds, int w,
-                                         int lane) {
-    const fi_i32x4 xr = make_rsrc(c.a2 + (size_t)f * 5184, 10368);
-    const fi_i32x4 dr = make_rsrc(c.da3 + (size_t)f * 3136, 6272);
-    const fi_i32x4 mr = make_rsrc(c.a3 + (size_t)f * 3136, 6272);
-    const uint32_t* tx = tab + 64 * w + lane;
-    const uint32_t* td = tab + 64 * (c3::NX + w) + lane;
-    uint32_t ox[3], od[4];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) ox[i] = tx[256 * i];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) od[i] = td[256 * i];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) blds16(xr, ox[i], slot_lds + (w + 4 * i) * 1024);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        blds16(dr, od[i], slot_lds + c3::XB + (w + 4 * i) * 1024);
-        blds16(mr, od[i], slot_lds + c3::XB + c3::DYB + (w + 4 * i) * 1024);
-    }
-}
-
 // Linear-DMA pipeline: every frame's a2, da3 and a3 arrive by LDS-DMA in their own byte order
 // (1 KiB contiguous per wave instruction) into one of two staging buffers; the issuing wave
 // then moves its own landed pieces into the frame's image slot (chunk-planar X, bordered dY),
 // applying the a3 ReLU mask to da3 on the way, so the mask image needs no slot. The gathered
-// DMA straight into the image layouts (FI_C3_GATHER) issued 16-byte pieces at a 128-byte
-// stride: the same bytes, 8x the memory requests (-DFI_EXP_LINDMA, linear sources with wrong
-// layouts: 4.29 -> 3.85 ms).
+// DMA straight into the image layouts issued 16-byte pieces at a 128-byte
+// stride: the same bytes, 8x the memory requests (timing with linear sources and wrong
+// layouts: 4.29 -> 3.85 ms; the gathered form is no longer built).
 // LDS: 2 image slots (X + dY, 28,672 B each; gap / border units zeroed once, never written),
 // 2 staging buffers (a2 11 + da3 7 + a3 7 pieces of 1 KiB), destination tables: 110,624 B.
 namespace c3 {

@@ -192,18 +192,35 @@ def test_bad_arguments_fail_loudly():
         L.step([b"\0" * 4096] * 15)  # wrong batch size
 
 
-def test_async_step_matches_sync_steps(orc):
+def oracle_sgd_trajectory(orc, L, raw_batches, p0, lr=1e-3):
+    """The oracle's view of len(raw_batches) SGD steps from p0: final parameters and the last
+    step's total loss (computed with the parameters before that step)."""
+    p = p0.astype(np.float32).copy()
+    tot = None
+    for b in raw_batches:
+        ref = oracle_step(orc, L, b, p)
+        tot = orc.total_loss(ref["vt"]["losses"])
+        p = (p - np.float32(lr) * ref["grads"].astype(np.float32)).astype(np.float32)
+    return p, tot
+
+
+@pytest.mark.parametrize("opt", ["adam", "sgd"])
+def test_async_step_matches_sync_steps(orc, opt):
     """fi_learner_step_async x4 (entries freed right after each call; both staging slots are
     reused, so the H2D of batch k+2 must wait for the ingest of batch k) then wait == four
-    synchronous steps on the same batches: same parameters, same last statistics."""
+    synchronous steps on the same batches: same parameters, same last statistics. With SGD the
+    run is also replayed through the oracle (forward, V-trace, backward, update per batch):
+    final parameters and the last step's loss match it."""
     from freeimpala_amd.learner import pack_records
     T, B = 6, 32
-    batches = []
+    batches, raw = [], []
     for seed in (21, 22, 23, 24):
         b = orc.synth_batch(seed, T=T, B=B, A=18, D=128)
+        raw.append(b)
         batches.append(pack_records(b["obs"], b["mu"], b["actions"], b["rewards"], b["discounts"],
                                     entry_size=T + 1))
-    L1, L2 = mk(T=T, B=B, seed=9, optimizer="adam"), mk(T=T, B=B, seed=9, optimizer="adam")
+    L1, L2 = mk(T=T, B=B, seed=9, optimizer=opt), mk(T=T, B=B, seed=9, optimizer=opt)
+    p0 = L2.get_params()
     for e in batches:
         s1 = L1.step(e)
     for e in batches:
@@ -213,22 +230,30 @@ def test_async_step_matches_sync_steps(orc):
     s2 = L2.wait()
     np.testing.assert_array_equal(L1.get_params(), L2.get_params())
     assert s1["total_loss"] == s2["total_loss"] and s1["version"] == s2["version"] == 4
+    if opt == "sgd":
+        p_ref, tot = oracle_sgd_trajectory(orc, L2, raw, p0)
+        scaled_close(L2.get_params(), p_ref, 1e-6, "params after 4 async steps vs oracle")
+        assert abs(s2["total_loss"] - tot) <= 1e-5 * max(1.0, abs(tot)), (s2["total_loss"], tot)
 
 
-def test_staged_steps_match_entry_steps(orc):
+@pytest.mark.parametrize("opt", ["adam", "sgd"])
+def test_staged_steps_match_entry_steps(orc, opt):
     """Zero-copy staging: batches written straight into the acquired pinned buffer (what
     SharedBuffer::readBatchInto would do), submitted sync and async, give the same parameters
     and statistics as fi_learner_step on the same entries. Submitting without an acquired
-    buffer is an error that leaves the handle usable."""
+    buffer is an error that leaves the handle usable. With SGD the five steps are also replayed
+    through the oracle: final parameters and the last loss match it."""
     from freeimpala_amd._abi import FiError
     from freeimpala_amd.learner import pack_records
     T, B = 6, 32
-    batches = []
+    batches, raw = [], []
     for seed in (31, 32, 33, 34, 35):
         b = orc.synth_batch(seed, T=T, B=B, A=18, D=128)
+        raw.append(b)
         batches.append(pack_records(b["obs"], b["mu"], b["actions"], b["rewards"], b["discounts"],
                                     entry_size=T + 2))  # one spare record: S > T+1
-    L1, L2 = mk(T=T, B=B, seed=4, optimizer="adam"), mk(T=T, B=B, seed=4, optimizer="adam")
+    L1, L2 = mk(T=T, B=B, seed=4, optimizer=opt), mk(T=T, B=B, seed=4, optimizer=opt)
+    p0 = L2.get_params()
     for e in batches:
         s1 = L1.step(e)
     with pytest.raises(FiError):
@@ -246,6 +271,10 @@ def test_staged_steps_match_entry_steps(orc):
     s2 = L2.wait()
     np.testing.assert_array_equal(L1.get_params(), L2.get_params())
     assert s1["total_loss"] == s2["total_loss"] and s1["version"] == s2["version"] == 5
+    if opt == "sgd":
+        p_ref, tot = oracle_sgd_trajectory(orc, L2, raw, p0)
+        scaled_close(L2.get_params(), p_ref, 1e-6, "params after 5 staged steps vs oracle")
+        assert abs(s2["total_loss"] - tot) <= 1e-5 * max(1.0, abs(tot)), (s2["total_loss"], tot)
 
 
 @pytest.mark.parametrize("arch", ["mlp", "atari"])
