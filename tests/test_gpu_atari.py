@@ -156,6 +156,33 @@ def test_atari_production_path_steady_state_parity(orc, T, B, grid, monkeypatch)
     L.close()
 
 
+@pytest.mark.parametrize("T,B,grid", [(2, 7, 4), (3, 32, 8)])
+def test_atari_own_fc_path_parity(orc, T, B, grid, monkeypatch):
+    """FI_FC_OWN=1: every fc GEMM on the hand-written kernels (forward with its bias + ReLU
+    epilogue, unmasked data gradient, weight gradient) on the production conv path, every stage
+    and gradient against the oracle. 21 frames: one partial row tile (rows past 21 read as zero
+    through the buffer descriptors, their stores dropped) and a single R-slice; 128 frames on
+    8 persistent workgroups."""
+    A = 18
+    for k in ("FI_KEEP_DA1", "FI_A1_NHWC", "FI_FWD_UNFUSED", "FI_BWD_UNFUSED"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("FI_FC_OWN", "1")
+    monkeypatch.setenv("FI_FR_GRID", str(grid))
+    N = (T + 1) * B
+    monkeypatch.setenv("FI_KEEP_DA1", "1")
+    twin = mk(T=T, B=B, A=A, seed=19)
+    monkeypatch.delenv("FI_KEEP_DA1")
+    L = mk(T=T, B=B, A=A, seed=19)
+    for x in (twin, L):
+        x.synth(seed=T * 977 + B)
+    twin.step_resident()
+    da1 = bf16_to_f32(twin.tensor("da1", np.uint16, (N, 20, 20, 32)))
+    g = _check_step_against_oracle(orc, L, T, B, A, a1_planar=True, da1=da1)
+    np.testing.assert_array_equal(g, twin.tensor("grads"))
+    twin.close()
+    L.close()
+
+
 def test_atari_training_reduces_loss():
     """gamma = 0 makes the V-trace target the (clipped) immediate reward, so the value loss of a
     fixed batch is a plain regression that SGD must reduce."""
