@@ -44,6 +44,8 @@ def kernel_work(arch, T, B, A, D=128, H=256):
             "mlp_fwd_l1": (2 * R * D * H, R * f32 * (D + H)), "mlp_fwd_l2": (2 * R * H * H, R * f32 * 2 * H),
             "mlp_fwd_heads": (2 * R * H * O, R * f32 * (H + O)), "mlp_wgrad_heads": (2 * R * H * O, R * f32 * (H + O)),
             "mlp_dgrad_heads": (2 * R * O * H, R * f32 * (O + 2 * H)), "mlp_wgrad_l2": (2 * R * H * H, R * f32 * 2 * H),
+            # fused heads backward: reads h2 and the upstream gradient once, writes dz2
+            "mlp_heads_bwd": (4 * R * H * O, R * f32 * (2 * H + O)),
             "mlp_dgrad_l2": (2 * R * H * H, R * f32 * 3 * H), "mlp_wgrad_l1": (2 * R * D * H, R * f32 * (D + H)),
         })
     else:

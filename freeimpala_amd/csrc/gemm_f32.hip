@@ -344,6 +344,87 @@ int f32_heads_wgrad_partial(const float* X, int I, const HeadsGrad& g, int split
     return launch(la, lb, EpiSlab{slab, N, (size_t)I * N}, I, N, g.rows, splits, s, cs_slab);
 }
 
+// ---- MLP heads backward, fused (H = 256, O = A + 1 outputs): one pass over h2 computes both
+// the heads' weight gradient (slab[block][H][O] = sum over the block's rows of h2[r][j] dout[r][o],
+// plus the bias partials sum_r dout[r][o]) and the data gradient dz2[r][j] = (h2[r][j] > 0) *
+// sum_o dout[r][o] Wh[j][o]. The two GEMM launches it replaces read h2 twice and ran the skinny
+// O = 19 side padded to a 64-wide MFMA tile (1.0 ms at R = 413,696 against a 0.85 GB memory
+// floor). A wave takes one row at a time (lane: 4 consecutive columns, the row's upstream
+// gradient in scalar registers), rows r = its global wave index + k * (all waves); the block's 4
+// waves are combined in a fixed order (deterministic), the blocks by reduce_slabs.
+template <int O>
+__global__ __launch_bounds__(256, 2) void heads_bwd_fused_f32(HeadsGrad g, const float* __restrict__ h2,
+                                                              const float* __restrict__ Wh,  // [256][O]
+                                                              float* __restrict__ dz2, float* __restrict__ slab,
+                                                              float* __restrict__ cs_slab) {
+    constexpr int H = 256, A = O - 1;
+    __shared__ float red[H * O];
+    __shared__ float bred[4][O];
+    const int lane = threadIdx.x & 63, w = wave_id(), j0 = 4 * lane;
+    float wv[4][O], acc[4][O], bs[O];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+        for (int o = 0; o < O; ++o) {
+            wv[jj][o] = Wh[(size_t)(j0 + jj) * O + o];
+            acc[jj][o] = 0.f;
+        }
+#pragma unroll
+    for (int o = 0; o < O; ++o) bs[o] = 0.f;
+    const int nw = gridDim.x * 4;
+    for (int r = blockIdx.x * 4 + w; r < g.rows; r += nw) {
+        float d[O];
+#pragma unroll
+        for (int o = 0; o < A; ++o) d[o] = r < g.TB ? g.dlog[(size_t)r * A + o] : 0.f;
+        d[A] = g.dval[r];
+        const float4 hv = *(const float4*)(h2 + (size_t)r * H + j0);
+        const float hx[4] = {hv.x, hv.y, hv.z, hv.w};
+        float dx[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            float a = 0.f;
+#pragma unroll
+            for (int o = 0; o < O; ++o) {
+                a = fmaf(d[o], wv[jj][o], a);
+                acc[jj][o] = fmaf(hx[jj], d[o], acc[jj][o]);
+            }
+            dx[jj] = hx[jj] > 0.f ? a : 0.f;
+        }
+        *(float4*)(dz2 + (size_t)r * H + j0) = make_float4(dx[0], dx[1], dx[2], dx[3]);
+#pragma unroll
+        for (int o = 0; o < O; ++o) bs[o] += d[o];
+    }
+    for (int i = threadIdx.x; i < H * O; i += 256) red[i] = 0.f;
+    __syncthreads();
+    for (int ww = 0; ww < 4; ++ww) {  // fixed-order combine of the block's waves
+        if (w == ww) {
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+                for (int o = 0; o < O; ++o) red[(j0 + jj) * O + o] += acc[jj][o];
+            if (lane == 0)
+#pragma unroll
+                for (int o = 0; o < O; ++o) bred[ww][o] = bs[o];
+        }
+        __syncthreads();
+    }
+    for (int i = threadIdx.x; i < H * O; i += 256) slab[(size_t)blockIdx.x * H * O + i] = red[i];
+    if (threadIdx.x < O)
+        cs_slab[(size_t)blockIdx.x * O + threadIdx.x] =
+            (bred[0][threadIdx.x] + bred[1][threadIdx.x]) + (bred[2][threadIdx.x] + bred[3][threadIdx.x]);
+}
+
+bool f32_heads_bwd_fused_supported(int H, int A) { return H == 256 && A == 18; }
+
+int f32_heads_bwd_fused(const HeadsGrad& g, const float* h2, const float* Wh, int H, float* dz2, float* slab,
+                        float* cs_slab, int grid, hipStream_t s) {
+    FI_REQUIRE(f32_heads_bwd_fused_supported(H, g.A), "heads_bwd_fused: H = 256, A = 18 only");
+    FI_REQUIRE(aligned16(h2) && aligned16(dz2), "heads_bwd_fused: 16-byte aligned h2 / dz2");
+    hipLaunchKernelGGL(heads_bwd_fused_f32<19>, dim3(grid), dim3(256), 0, s, g, h2, Wh, dz2, slab, cs_slab);
+    FI_HIP_CHECK(hipGetLastError());
+    return FI_OK;
+}
+
 // ---- PyTorch-layout weights (W[N][K], nn.Linear): the FarmerLstm torso (farmer.hip)
 // Y[M][N] = X[M][K] W[N][K]^T + b (ReLU); ldx = row stride of X
 int f32_gemm_nt(const float* X, int ldx, int M, int K, const float* W, const float* bias, int N,

@@ -44,6 +44,12 @@ int f32_linear_wgrad_partial(const float* X, int M, int I, const float* dY, int 
                              float* slab, float* cs_slab, hipStream_t s);
 int f32_heads_wgrad_partial(const float* X, int I, const HeadsGrad& g, int splits, float* slab,
                             float* cs_slab, hipStream_t s);
+// heads weight gradient (slab [grid][H][A+1] + bias partials [grid][A+1]) and masked data
+// gradient dz2 in one pass over h2 (H = 256, A = 18)
+bool f32_heads_bwd_fused_supported(int H, int A);
+constexpr int kHeadsFusedGrid = 512;
+int f32_heads_bwd_fused(const HeadsGrad& g, const float* h2, const float* Wh, int H, float* dz2, float* slab,
+                        float* cs_slab, int grid, hipStream_t s);
 
 // misc.hip
 int colsum_partial(const float* Y, int M, int N, int splits, float* slab, hipStream_t s);

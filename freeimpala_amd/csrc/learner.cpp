@@ -476,11 +476,20 @@ static int mlp_backward(fi_learner* l, GradReadyHook* gr) {
     float* gbh = gWh + (size_t)H * O;
     HeadsGrad g{l->dlogits, l->dvalue, l->rows, l->TB, A};
     float* cs = l->slab + l->slab_floats - (size_t)l->splits * 4096;
-    { Tag t(l, "mlp_wgrad_heads"); FI_TRY(f32_heads_wgrad_partial(l->h2, H, g, l->splits, l->slab, cs, l->stream)); }
-    { Tag t(l, "reduce_slabs"); FI_TRY(reduce_slabs(l->slab, l->splits, (size_t)H * O, gWh, l->stream)); }
-    { Tag t(l, "reduce_slabs"); FI_TRY(reduce_slabs(cs, l->splits, (size_t)O, gbh, l->stream)); }
-    FI_TRY(gr->ready((size_t)(gWh - l->grads), (size_t)H * O + O));
-    { Tag t(l, "mlp_dgrad_heads"); FI_TRY(f32_heads_dgrad(g, Wh, H, l->h2, l->dz2, l->stream)); }
+    if (f32_heads_bwd_fused_supported(H, A) && (size_t)kHeadsFusedGrid * (H * O + O) <= l->slab_floats) {
+        // both heads gradients in one pass over h2 (weight-gradient slabs, then dz2)
+        float* hcs = l->slab + (size_t)kHeadsFusedGrid * H * O;
+        { Tag t(l, "mlp_heads_bwd"); FI_TRY(f32_heads_bwd_fused(g, l->h2, Wh, H, l->dz2, l->slab, hcs, kHeadsFusedGrid, l->stream)); }
+        { Tag t(l, "reduce_slabs"); FI_TRY(reduce_slabs(l->slab, kHeadsFusedGrid, (size_t)H * O, gWh, l->stream)); }
+        { Tag t(l, "reduce_slabs"); FI_TRY(reduce_slabs(hcs, kHeadsFusedGrid, (size_t)O, gbh, l->stream)); }
+        FI_TRY(gr->ready((size_t)(gWh - l->grads), (size_t)H * O + O));
+    } else {
+        { Tag t(l, "mlp_wgrad_heads"); FI_TRY(f32_heads_wgrad_partial(l->h2, H, g, l->splits, l->slab, cs, l->stream)); }
+        { Tag t(l, "reduce_slabs"); FI_TRY(reduce_slabs(l->slab, l->splits, (size_t)H * O, gWh, l->stream)); }
+        { Tag t(l, "reduce_slabs"); FI_TRY(reduce_slabs(cs, l->splits, (size_t)O, gbh, l->stream)); }
+        FI_TRY(gr->ready((size_t)(gWh - l->grads), (size_t)H * O + O));
+        { Tag t(l, "mlp_dgrad_heads"); FI_TRY(f32_heads_dgrad(g, Wh, H, l->h2, l->dz2, l->stream)); }
+    }
     FI_TRY(wgrad(l, "mlp_wgrad_l2", l->h1, H, l->dz2, H, gW2, gb2));
     FI_TRY(gr->ready((size_t)(gW2 - l->grads), (size_t)H * H + H));
     { Tag t(l, "mlp_dgrad_l2"); FI_TRY(f32_linear_dgrad(l->dz2, l->rows, H, W2, H, l->h1, l->dz1, l->stream)); }
