@@ -372,12 +372,20 @@ __global__ __launch_bounds__(256, 2) void heads_bwd_fused_f32(HeadsGrad g, const
 #pragma unroll
     for (int o = 0; o < O; ++o) bs[o] = 0.f;
     const int nw = gridDim.x * 4;
-    for (int r = blockIdx.x * 4 + w; r < g.rows; r += nw) {
-        float d[O];
+    auto row_in = [&](int r, float (&d)[O], float4& hv) {
 #pragma unroll
         for (int o = 0; o < A; ++o) d[o] = r < g.TB ? g.dlog[(size_t)r * A + o] : 0.f;
         d[A] = g.dval[r];
-        const float4 hv = *(const float4*)(h2 + (size_t)r * H + j0);
+        hv = *(const float4*)(h2 + (size_t)r * H + j0);
+    };
+    int r = blockIdx.x * 4 + w;
+    float d[O];
+    float4 hv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r < g.rows) row_in(r, d, hv);
+    for (; r < g.rows; r += nw) {
+        float dn[O];  // the next row's inputs, loaded while this row computes
+        float4 hn = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (r + nw < g.rows) row_in(r + nw, dn, hn);
         const float hx[4] = {hv.x, hv.y, hv.z, hv.w};
         float dx[4];
 #pragma unroll
@@ -392,7 +400,11 @@ __global__ __launch_bounds__(256, 2) void heads_bwd_fused_f32(HeadsGrad g, const
         }
         *(float4*)(dz2 + (size_t)r * H + j0) = make_float4(dx[0], dx[1], dx[2], dx[3]);
 #pragma unroll
-        for (int o = 0; o < O; ++o) bs[o] += d[o];
+        for (int o = 0; o < O; ++o) {
+            bs[o] += d[o];
+            d[o] = dn[o];
+        }
+        hv = hn;
     }
     for (int i = threadIdx.x; i < H * O; i += 256) red[i] = 0.f;
     __syncthreads();
