@@ -110,8 +110,8 @@ struct EpiBf16Out {
 struct EpiFwd : EpiBf16Out<FCO> {  // h[y][x] = bf16(relu(v + b[x])); bias in LDS (no VMEM in the loop)
     const float* bias;  // [512], copied into LDS at kernel start
     static constexpr int kLdsFloats = FCO;
-    __device__ void init(float* lds_f, int tid) const {
-        for (int i = tid; i < FCO; i += 512) lds_f[i] = bias[i];
+    __device__ void init(float* lds_f, int tid, int nthr) const {
+        for (int i = tid; i < FCO; i += nthr) lds_f[i] = bias[i];
     }
     __device__ static i32x2 act(const float* lb, int x, f32x4 v) {
         const f32x4 b = *(const f32x4*)(lb + x);
@@ -129,7 +129,7 @@ struct EpiFwd : EpiBf16Out<FCO> {  // h[y][x] = bf16(relu(v + b[x])); bias in LD
 };
 struct EpiDgrad : EpiBf16Out<FCK> {  // da3[y][x] = bf16(v) (unmasked: conv3's backward applies the a3 mask)
     static constexpr int kLdsFloats = 0;
-    __device__ void init(float*, int) const {}
+    __device__ void init(float*, int, int) const {}
     __device__ static i32x2 cvt(f32x4 v) { return i32x2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])}; }
     template <int AUX>
     __device__ static void pair(const OutTile& o, const float*, int xf, int y, int G, f32x4 v0, f32x4 v1) {
@@ -152,20 +152,23 @@ __device__ __forceinline__ int nt_chunk(int c, int row) {
 }
 
 // ---------------------------------------------------------------- NT kernel
-// OPT bits: 1 = s_setprio 1 around each MFMA cluster, 2 = nontemporal (streaming) output stores
+// OPT bits: 1 = s_setprio 1 around each MFMA cluster, 2 = nontemporal (streaming) output stores,
+// 4 = accumulators in AGPRs (for 4-wave tiles of 128 x 128 per wave)
 template <int BX, int BY, int WX, int WY, int BK, int NS, class Epi, int OPT = 0>
-__global__ __launch_bounds__(512) void fc_nt_kernel(const __bf16* __restrict__ X, const __bf16* __restrict__ Y,
+__global__ __launch_bounds__(64 * WX * WY) void fc_nt_kernel(const __bf16* __restrict__ X, const __bf16* __restrict__ Y,
                                                     int NY, int K, int ntx, int ntiles, Epi epi) {
     constexpr int TX = BX / WX, TY = BY / WY, FX = TX / 16, FY = TY / 16;
     constexpr int RPP = 1024 / (BK * 2);                      // image rows per 1-KiB DMA piece
-    constexpr int PX = BX / RPP, P = (BX + BY) / RPP, PW = (P + 7) / 8;
+    constexpr int NW = WX * WY;                               // waves
+    constexpr int PX = BX / RPP, P = (BX + BY) / RPP, PW = (P + NW - 1) / NW;
     constexpr int SLOT = (BX + BY) * BK * 2;
     constexpr int NST = FY * (FX / 2 + FX % 2);               // epilogue stores per wave
     constexpr int D = NS - 1;                                 // steps in flight ahead
     constexpr int AUX = (OPT & 2) ? 2 : 0;
-    static_assert(WX * WY == 8 && FX * 16 == TX && FY * 16 == TY && (BK == 64 || BK == 32), "tile");
+    static_assert((NW == 8 || NW == 4) && FX * 16 == TX && FY * 16 == TY && (BK == 64 || BK == 32), "tile");
     static_assert(BX % RPP == 0 && BY % RPP == 0 && (D - 1) * PW + NST < 64, "ring");
     __shared__ __attribute__((aligned(16))) char lds[NS * SLOT + Epi::kLdsFloats * 4];
+    if constexpr (OPT & 4) asm volatile("" ::"a"(0));  // AGPR-form MFMAs: accumulators in AGPRs
     const int lane = threadIdx.x & 63, w = wave_id(), G = lane >> 4;
     const int wx = w / WY, wy = w % WY;
     const int NG = gridDim.x, lg = xcd_remap(blockIdx.x, NG);
@@ -173,7 +176,7 @@ __global__ __launch_bounds__(512) void fc_nt_kernel(const __bf16* __restrict__ X
     const int total = ((ntiles - 1 - lg) / NG + 1) * nk;
     const uint32_t lbase = lds_addr(lds);
     const float* lb = (const float*)(lds + NS * SLOT);
-    epi.init((float*)(lds + NS * SLOT), threadIdx.x);
+    epi.init((float*)(lds + NS * SLOT), threadIdx.x, 64 * NW);
 
     int is_tile = 0, is_kt = 0;  // the next step to issue (tile index of this workgroup, k-step)
     auto issue = [&](int it) {   // this wave's 1-KiB pieces of step `it` into slot it % NS
@@ -185,8 +188,8 @@ __global__ __launch_bounds__(512) void fc_nt_kernel(const __bf16* __restrict__ X
         const uint32_t sb = lbase + (uint32_t)(it % NS) * SLOT;
 #pragma unroll
         for (int i = 0; i < PW; ++i) {
-            int pi = w + 8 * i;
-            if (pi >= P) pi -= 8;  // uneven piece count: a duplicate (same bytes, same place)
+            int pi = w + NW * i;
+            if (pi >= P) pi -= NW;  // uneven piece count: a duplicate (same bytes, same place)
             const bool isx = pi < PX;
             const int prow = (isx ? pi : pi - PX) * RPP + lane / (BK / 8);
             const int ch = nt_chunk<BK>(lane % (BK / 8), prow);
@@ -195,67 +198,64 @@ __global__ __launch_bounds__(512) void fc_nt_kernel(const __bf16* __restrict__ X
         if (++is_kt == nk) is_kt = 0, ++is_tile;
     };
 
-    f32x4 acc[FX][FY];
-#pragma unroll
-    for (int f = 0; f < FX; ++f)
-#pragma unroll
-        for (int g = 0; g < FY; ++g) acc[f][g] = f32x4{0.f, 0.f, 0.f, 0.f};
-
     for (int d = 0; d < D && d < total; ++d) issue(d);
-    int kt = 0, tile_it = 0, last_epi = -(1 << 20);
-    for (int it = 0; it < total; ++it) {
-        // younger than this step's loads: the steps issued after it (at most D-1), and the
-        // last epilogue's stores if they were issued after this step's loads
-        const int ahead = min(D - 1, total - 1 - it);
-        vm_wait_rt(ahead * PW + (it - last_epi <= D ? NST : 0));
-        lds_barrier();
-        if (it + D < total) issue(it + D);
-        const char* sx = lds + (it % NS) * SLOT;
-        const char* sy = sx + BX * BK * 2;
+    // tile-outer / k-inner: the accumulators are zeroed per tile outside the k loop (a reset
+    // inside it would merge two definitions at the loop head: with AGPR accumulators the
+    // compiler then copies every accumulator through VGPRs each step)
+    const int mytiles = total / nk;
+    int it = 0, last_epi = -(1 << 20);
+    for (int tile_it = 0; tile_it < mytiles; ++tile_it) {
+        f32x4 acc[FX][FY];
 #pragma unroll
-        for (int s = 0; s < BK / 32; ++s) {
-            const int ch = s * 4 + G;
-            bf16x8 fa[FX], fb[FY];
+        for (int f = 0; f < FX; ++f)
 #pragma unroll
-            for (int f = 0; f < FX; ++f) {
-                const int row = wx * TX + f * 16 + (lane & 15);
-                fa[f] = *(const bf16x8*)(sx + row * (BK * 2) + (nt_chunk<BK>(ch, row) << 4));
+            for (int g = 0; g < FY; ++g) acc[f][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int kt = 0; kt < nk; ++kt, ++it) {
+            // younger than this step's loads: the steps issued after it (at most D-1), and the
+            // last epilogue's stores if they were issued after this step's loads
+            const int ahead = min(D - 1, total - 1 - it);
+            vm_wait_rt(ahead * PW + (it - last_epi <= D ? NST : 0));
+            lds_barrier();
+            if (it + D < total) issue(it + D);
+            const char* sx = lds + (it % NS) * SLOT;
+            const char* sy = sx + BX * BK * 2;
+#pragma unroll
+            for (int s = 0; s < BK / 32; ++s) {
+                const int ch = s * 4 + G;
+                bf16x8 fa[FX], fb[FY];
+#pragma unroll
+                for (int f = 0; f < FX; ++f) {
+                    const int row = wx * TX + f * 16 + (lane & 15);
+                    fa[f] = *(const bf16x8*)(sx + row * (BK * 2) + (nt_chunk<BK>(ch, row) << 4));
+                }
+#pragma unroll
+                for (int g = 0; g < FY; ++g) {
+                    const int row = wy * TY + g * 16 + (lane & 15);
+                    fb[g] = *(const bf16x8*)(sy + row * (BK * 2) + (nt_chunk<BK>(ch, row) << 4));
+                }
+                if constexpr (OPT & 1) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+                for (int f = 0; f < FX; ++f)
+#pragma unroll
+                    for (int g = 0; g < FY; ++g)
+                        acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[f], fb[g], acc[f][g], 0, 0, 0);
+                if constexpr (OPT & 1) __builtin_amdgcn_s_setprio(0);
             }
-#pragma unroll
-            for (int g = 0; g < FY; ++g) {
-                const int row = wy * TY + g * 16 + (lane & 15);
-                fb[g] = *(const bf16x8*)(sy + row * (BK * 2) + (nt_chunk<BK>(ch, row) << 4));
-            }
-            if constexpr (OPT & 1) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-            for (int f = 0; f < FX; ++f)
-#pragma unroll
-                for (int g = 0; g < FY; ++g)
-                    acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[f], fb[g], acc[f][g], 0, 0, 0);
-            if constexpr (OPT & 1) __builtin_amdgcn_s_setprio(0);
         }
-        if (++kt == nk) {
-            const int t = lg + tile_it * NG;
-            const int ty = t / ntx, tx = t - ty * ntx;
-            const int y0 = ty * BY;
-            const OutTile ot = epi.tile(y0, min(BY, NY - y0));
-            const int xw = tx * BX + wx * TX, yb = y0 + wy * TY + (lane & 15);
+        const int t = lg + tile_it * NG;
+        const int ty = t / ntx, tx = t - ty * ntx;
+        const int y0 = ty * BY;
+        const OutTile ot = epi.tile(y0, min(BY, NY - y0));
+        const int xw = tx * BX + wx * TX, yb = y0 + wy * TY + (lane & 15);
 #pragma unroll
-            for (int g = 0; g < FY; ++g) {
+        for (int g = 0; g < FY; ++g) {
 #pragma unroll
-                for (int f = 0; f + 1 < FX; f += 2)
-                    Epi::template pair<AUX>(ot, lb, xw + f * 16, yb + g * 16, G, acc[f][g], acc[f + 1][g]);
-                if constexpr (FX % 2)
-                    Epi::template single<AUX>(ot, lb, xw + (FX - 1) * 16, yb + g * 16, G, acc[FX - 1][g]);
-            }
-#pragma unroll
-            for (int f = 0; f < FX; ++f)
-#pragma unroll
-                for (int g = 0; g < FY; ++g) acc[f][g] = f32x4{0.f, 0.f, 0.f, 0.f};
-            kt = 0;
-            ++tile_it;
-            last_epi = it;
+            for (int f = 0; f + 1 < FX; f += 2)
+                Epi::template pair<AUX>(ot, lb, xw + f * 16, yb + g * 16, G, acc[f][g], acc[f + 1][g]);
+            if constexpr (FX % 2)
+                Epi::template single<AUX>(ot, lb, xw + (FX - 1) * 16, yb + g * 16, G, acc[FX - 1][g]);
         }
+        last_epi = it - 1;
     }
 }
 
@@ -382,7 +382,7 @@ template <int BX, int BY, int WX, int WY, int BK, int NS, int OPT = 0>
 static int fc_fwd_impl(const __bf16* a3, const __bf16* wT, const float* bias, __bf16* h, int rows, hipStream_t s) {
     FI_REQUIRE(rows > 0, "fc_fwd: rows must be positive");
     const int ntx = FCO / BX, nty = (rows + BY - 1) / BY, nt = ntx * nty;
-    hipLaunchKernelGGL((fc_nt_kernel<BX, BY, WX, WY, BK, NS, EpiFwd, OPT>), dim3(std::min(nt, 256)), dim3(512), 0, s, wT, a3,
+    hipLaunchKernelGGL((fc_nt_kernel<BX, BY, WX, WY, BK, NS, EpiFwd, OPT>), dim3(std::min(nt, 256)), dim3(64 * WX * WY), 0, s, wT, a3,
                            rows, FCK, ntx, nt, EpiFwd{{h}, bias});
     FI_HIP_CHECK(hipGetLastError());
     return FI_OK;
@@ -392,7 +392,7 @@ template <int BX, int BY, int WX, int WY, int BK, int NS, int OPT = 0>
 static int fc_dgrad_impl(const __bf16* dh, const __bf16* w, __bf16* da3, int rows, hipStream_t s) {
     FI_REQUIRE(rows > 0, "fc_dgrad: rows must be positive");
     const int ntx = FCK / BX, nty = (rows + BY - 1) / BY, nt = ntx * nty;
-    hipLaunchKernelGGL((fc_nt_kernel<BX, BY, WX, WY, BK, NS, EpiDgrad, OPT>), dim3(std::min(nt, 256)), dim3(512), 0, s, w,
+    hipLaunchKernelGGL((fc_nt_kernel<BX, BY, WX, WY, BK, NS, EpiDgrad, OPT>), dim3(std::min(nt, 256)), dim3(64 * WX * WY), 0, s, w,
                            dh, rows, FCO, ntx, nt, EpiDgrad{{da3}});
     FI_HIP_CHECK(hipGetLastError());
     return FI_OK;

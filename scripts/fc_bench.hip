@@ -76,11 +76,13 @@ int main(int argc, char** argv) {
 #define WGV(nm, S, ...) add("wgrd " nm, 2, [&](hipStream_t st, int k) { return fc_wgrad_impl<__VA_ARGS__>(a3, dh, slab, dw[k], R, st, S); }, dw[0], dw[1], (size_t)FCK * FCO * 4)
     // the shipped configurations first (fc_gemm.hip FC_*_CFG), then alternatives
     FWDV("256x256 w4x2 bk64 ns2 prio", 256, 256, 4, 2, 64, 2, 1);
-    FWDV("256x256 w2x4 bk64 ns2", 256, 256, 2, 4, 64, 2, 0);
-    FWDV("256x256 w2x4 bk32 ns4", 256, 256, 2, 4, 32, 4, 0);
+    FWDV("256x256 w2x2 bk64 ns2 agpr", 256, 256, 2, 2, 64, 2, 4);
+    FWDV("256x256 w2x2 bk64 ns2 agpr prio", 256, 256, 2, 2, 64, 2, 5);
+    FWDV("256x256 w2x2 bk32 ns4 agpr", 256, 256, 2, 2, 32, 4, 4);
     DGV("224x256 w1x8 bk64 ns2 prio", 224, 256, 1, 8, 64, 2, 1);
-    DGV("224x256 w2x4 bk64 ns2", 224, 256, 2, 4, 64, 2, 0);
-    DGV("224x256 w1x8 bk64 ns2 prio nt", 224, 256, 1, 8, 64, 2, 3);
+    DGV("224x256 w2x2 bk64 ns2 agpr", 224, 256, 2, 2, 64, 2, 4);
+    DGV("224x256 w1x4 bk64 ns2 agpr", 224, 256, 1, 4, 64, 2, 4);
+    DGV("224x256 w2x2 bk32 ns4 agpr", 224, 256, 2, 2, 32, 4, 4);
     WGV("256x224 w4x2 bk64 ns2", 9, 256, 224, 4, 2, 64, 2);
     WGV("256x224 w4x2 bk32 ns4", 9, 256, 224, 4, 2, 32, 4);
     std::vector<std::vector<float>> ms(vs.size());
