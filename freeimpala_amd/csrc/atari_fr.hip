@@ -516,6 +516,15 @@ __device__ __forceinline__ int f3_dst(int i) {
     const int p = i >> 3, c = i & 7;
     return p < 81 ? p + 96 * c + fz(c) : 0;
 }
+// Reshuffle lane order for the pixel-major (8 chunks per pixel) conv3 inputs: lane L moves
+// unit rs_lane(L) of a 64-unit piece. In the identity order the 8 lanes of a ds_write_b128
+// bank group (8 contiguous lanes, bank (a/4) mod 32) hold one pixel's 8 chunks, whose image
+// units p + 96c + fz(c) fall on 2 distinct 16-B bank slots: 4-way conflicts (the conv3
+// kernels' SQ_LDS_BANK_CONFLICT). This order gives each write group 8 pixels of one chunk
+// pair pattern -- 8 distinct slots -- and keeps the staging ds_read_b128 groups conflict-free
+// (scripts/lds_conflicts.py model: 331 -> 88 LDS cycles per frame for the X image; the
+// bordered dY image 203 -> 104).
+__device__ __forceinline__ int rs_lane(int L) { return 8 * (L & 7) + ((2 * (L & 7) + (L >> 3)) & 7); }
 
 template <int L>  // L = 2 (conv2) or 3 (conv3)
 struct FwdGeo;
@@ -601,6 +610,7 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
     };
     // the issuing wave moves its own landed pieces of iteration i2 into image slot i2 & 1
     // (all reads first, then all writes: one LDS round trip, not one per piece)
+    const int sl = L == 3 ? rs_lane(lane) : lane;  // conv3: bank-conflict-free write groups
     auto reshuffle = [&](int i2) {
         u32x4 d[FPI][PPW];
         int du[FPI][PPW];
@@ -609,8 +619,8 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
 #pragma unroll
             for (int i = 0; i < PPW; ++i) {
                 const int j = min(w + 8 * i, NLP - 1);
-                d[u][i] = *(const u32x4*)(smem + IMG + (i2 % STG) * SBUF + u * NLP * 1024 + 1024 * j + 16 * lane);
-                du[u][i] = dstu[64 * j + lane];
+                d[u][i] = *(const u32x4*)(smem + IMG + (i2 % STG) * SBUF + u * NLP * 1024 + 1024 * j + 16 * sl);
+                du[u][i] = dstu[64 * j + sl];
             }
 #pragma unroll
         for (int u = 0; u < FPI; ++u) {
@@ -619,7 +629,7 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
                 char* im = smem + ((i2 & 1) * FPI + u) * G::XB;
 #pragma unroll
                 for (int i = 0; i < PPW; ++i) {
-                    const int j = w + 8 * i, b = 1024 * j + 16 * lane;
+                    const int j = w + 8 * i, b = 1024 * j + 16 * sl;
                     if (j < NLP && b < G::IN_BYTES) *(u32x4*)(im + 16 * du[u][i]) = d[u][i];
                 }
             }
@@ -1795,6 +1805,7 @@ __device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, int nst, W
         }
         return n;
     };
+    const int sl = rs_lane(lane);  // lane order with bank-conflict-free write groups
     auto reshuffle = [&](int sb, int slot) {  // own landed pieces -> image slot (a2, then da3: reads, then writes)
         const char* st = smem + c3::O_STG + sb * c3::STGB;
         char* im = smem + slot * c3::SLOT2;
@@ -1803,26 +1814,26 @@ __device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, int nst, W
             int xd[3];
 #pragma unroll
             for (int i = 0; i < 3; ++i) {
-                const int u = min(64 * (w + 4 * i) + lane, c3::NUX - 1);
+                const int u = min(64 * (w + 4 * i) + sl, c3::NUX - 1);
                 xv[i] = *(const u32x4*)(st + 16 * u);
                 xd[i] = dstx[u];
             }
 #pragma unroll
             for (int i = 0; i < 3; ++i)
-                if (64 * (w + 4 * i) + lane < c3::NUX) *(u32x4*)(im + 16 * xd[i]) = xv[i];
+                if (64 * (w + 4 * i) + sl < c3::NUX) *(u32x4*)(im + 16 * xd[i]) = xv[i];
         }
         s16x8 dv[2], mv[2];
         int dd[2];
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-            const int u = min(64 * (w + 4 * i) + lane, c3::NUD - 1);
+            const int u = min(64 * (w + 4 * i) + sl, c3::NUD - 1);
             dv[i] = *(const s16x8*)(st + 1024 * c3::NPX + 16 * u);
             mv[i] = *(const s16x8*)(st + 1024 * (c3::NPX + c3::NPD) + 16 * u);
             dd[i] = dsty[u];
         }
 #pragma unroll
         for (int i = 0; i < 2; ++i)
-            if (64 * (w + 4 * i) + lane < c3::NUD) {
+            if (64 * (w + 4 * i) + sl < c3::NUD) {
                 s16x8 v = dv[i];
 #pragma unroll
                 for (int q = 0; q < 8; ++q) v[q] = mv[i][q] > 0 ? v[q] : (short)0;
