@@ -204,10 +204,14 @@ struct EpiSlab {  // split-K partial slab: C[split][m][n]
     float* C;
     int ldc;
     size_t split_stride;
+    int z = 0;  // this workgroup's split (set by the kernel)
     __device__ void operator()(int m, int n, float v) const {
-        C[blockIdx.z * split_stride + (size_t)m * ldc + n] = v;
+        C[z * split_stride + (size_t)m * ldc + n] = v;
     }
 };
+template <class E>
+__device__ __forceinline__ void epi_set_split(E&, int) {}
+__device__ __forceinline__ void epi_set_split(EpiSlab& e, int z) { e.z = z; }
 
 // ---------------- the kernel --------------------------------------------------------
 // COLSUM: blocks of the first M-tile also sum the B tile over k (the bias gradient of a
@@ -218,12 +222,20 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(LA la, LB lb, Epi epi,
     __shared__ __attribute__((aligned(16))) float As[2][GBK * GLDA];
     __shared__ __attribute__((aligned(16))) float Bs[2][GBK * GLDB];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int m0 = blockIdx.x * GBM, n0 = blockIdx.y * GBN;
-    const int kbeg = blockIdx.z * k_per_split;
+    // tile order: the N-tiles of one (M-tile, split) get consecutive logical ids on ONE XCD
+    // (xcd_remap), so the A rows they share are fetched from HBM once and hit that XCD's L2
+    // for the others (in launch order they were gridDim.x workgroups apart)
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int lin = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const int lg = xcd_remap(lin, gx * gy * gridDim.z);
+    const int by = lg % gy, bx = (lg / gy) % gx, bz = lg / (gx * gy);
+    epi_set_split(epi, bz);
+    const int m0 = bx * GBM, n0 = by * GBN;
+    const int kbeg = bz * k_per_split;
     const int kend = min(K, kbeg + k_per_split);
     f32x16 acc0 = {}, acc1 = {};
     float cs = 0.f;
-    const bool do_cs = COLSUM && blockIdx.x == 0 && threadIdx.x < GBN;
+    const bool do_cs = COLSUM && bx == 0 && threadIdx.x < GBN;
     typename RegsOf<LA>::type ra[RegsOf<LA>::N];
     typename RegsOf<LB>::type rb[RegsOf<LB>::N];
     int buf = 0;
@@ -262,7 +274,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(LA la, LB lb, Epi epi,
         __syncthreads();
         buf ^= 1;
     }
-    if (do_cs && n0 + (int)threadIdx.x < N) colsum[(size_t)blockIdx.z * N + n0 + threadIdx.x] = cs;
+    if (do_cs && n0 + (int)threadIdx.x < N) colsum[(size_t)bz * N + n0 + threadIdx.x] = cs;
     // C/D map of 32x32 tiles: row = (r&3) + 8*(r>>2) + 4*(lane>>5), col = lane&31
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
