@@ -274,7 +274,11 @@ static int create(const fi_learner_config* cfg, fi_learner** out) {
         FI_TRY(dalloc_n(l, &l->h2, rows * H));
         FI_TRY(dalloc_n(l, &l->dz1, rows * H));
         FI_TRY(dalloc_n(l, &l->dz2, rows * H));
-        l->splits = (int)std::min<size_t>(128, std::max<size_t>(1, rows / 2048));
+        // weight-gradient R-slices: 384 at R = 413,696 gives the K = 128 layer 1,536 workgroups
+        // (6 per CU, the kernel's occupancy) -- with 128 its 512 workgroups left the CUs
+        // latency-bound (wgrad_l1 0.44 -> 0.29 ms, wgrad_l2 0.60 -> 0.54 ms; 512 slices measured
+        // slower: the slab sums grow)
+        l->splits = (int)std::min<size_t>(384, std::max<size_t>(1, rows / 1024));
         const size_t big = std::max<size_t>((size_t)D * H, (size_t)H * H);
         l->slab_floats = (size_t)l->splits * (big + 4096);  // wgrad slabs | bias colsum slabs
         FI_TRY(dalloc_n(l, &l->slab, l->slab_floats));
