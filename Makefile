@@ -55,6 +55,16 @@ build/mpi_pool_check: tests/cpp/mpi_pool_check.cpp $(wildcard include/freeimpala
 	g++ -std=c++17 -O2 -Wall -Wextra -Iinclude -I$(MPI_HOME)/include $< -o $@ -pthread $(MPI_LINK)
 host: build/mpi_pool_check
 
+# INTEGRATION.md section 2's alias compiled on the reference's own classes (build container only:
+# the reference tree is read in place, never copied; the binary travels to the GPU box)
+REF ?= /root/reference
+ifneq ($(wildcard $(REF)/include/freeimpala/data_structures.h),)
+host: build/reference_binding
+endif
+build/reference_binding: tests/cpp/reference_binding.cpp tests/cpp/stubs/spdlog/spdlog.h $(wildcard include/freeimpala_amd/*.hpp) include/fi_learner.h $(LIBDIR)/libfi_learner.so
+	@mkdir -p build
+	g++ -std=c++17 -O2 -Wall -I$(REF)/include -Itests/cpp/stubs -Iinclude -include optional $< -o $@ -L$(LIBDIR) -lfi_learner -pthread '-Wl,-rpath,$$ORIGIN/../$(LIBDIR)' -Wl,-rpath,/opt/rocm/lib
+
 clean:
 	rm -rf build $(LIBDIR)
 .PHONY: all oracle host tools clean

@@ -101,6 +101,7 @@ struct fi_learner {
     hipStream_t comm_stream = nullptr;
     std::vector<hipEvent_t> bucket_ev;
     hipEvent_t comm_done = nullptr;
+    hipEvent_t bad_ready = nullptr;  // orders the reject-flag all-reduce when no bucket ran
     int buckets = 0;  // buckets issued in the last step (introspection)
     // bookkeeping
     uint64_t version = 0;
@@ -199,6 +200,7 @@ static void destroy(fi_learner* l) {
     if (l->comm) ncclCommDestroy(l->comm);
     for (hipEvent_t e : l->bucket_ev) hipEventDestroy(e);
     if (l->comm_done) hipEventDestroy(l->comm_done);
+    if (l->bad_ready) hipEventDestroy(l->bad_ready);
     if (l->comm_stream) hipStreamDestroy(l->comm_stream);
     atari_destroy(l->atari);
     for (void* p : l->allocs) hipFree(p);
@@ -435,10 +437,23 @@ struct BucketAllReduce : GradReadyHook {
         if (r != ncclSuccess) return fail(FI_ERR_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
         return FI_OK;
     }
-    // the compute stream waits for every bucket before the optimizer reads the gradients
+    // The reject decision is agreed before anything is applied: after the last bucket the
+    // int counter of out-of-range actions (written by ingest and the V-trace kernel, both
+    // ordered before the first bucket's event) is summed over the ranks on the same stream,
+    // so the optimizer of EVERY replica sees the group's count and all of them skip the
+    // update together -- a shard's gradient from clamped actions is in the summed gradient,
+    // and no replica may apply it (reference log-and-skip: data_structures.h:420-421,
+    // agent.h:88-91). The compute stream then waits for every bucket before the optimizer
+    // reads the gradients.
     int join() {
         l->buckets = n;
-        if (!l->comm || n == 0) return FI_OK;
+        if (!l->comm) return FI_OK;
+        if (n == 0) {  // a backward without buckets still has to agree on the reject flag
+            FI_HIP_CHECK(hipEventRecord(l->bad_ready, l->stream));
+            FI_HIP_CHECK(hipStreamWaitEvent(l->comm_stream, l->bad_ready, 0));
+        }
+        ncclResult_t r = ncclAllReduce(l->bad, l->bad, 1, ncclInt32, ncclSum, l->comm, l->comm_stream);
+        if (r != ncclSuccess) return fail(FI_ERR_COMM, std::string("ncclAllReduce(reject flag): ") + ncclGetErrorString(r));
         FI_HIP_CHECK(hipEventRecord(l->comm_done, l->comm_stream));
         FI_HIP_CHECK(hipStreamWaitEvent(l->stream, l->comm_done, 0));
         return FI_OK;
@@ -513,6 +528,11 @@ static int check_rejected(fi_learner* l) {
     if (bad == 0) return FI_OK;
     l->step_count--;
     l->version--;
+    if (l->comm && l->nranks > 1)
+        return fail(FI_ERR_INVALID, "step: " + std::to_string(bad) + " action(s) outside [0, " +
+                                        std::to_string(l->A) + ") in the data-parallel group's batch "
+                                        "(all-reduced reject flag); batch rejected on every replica, "
+                                        "parameters unchanged");
     return fail(FI_ERR_INVALID, "step: " + std::to_string(bad) + " action(s) outside [0, " +
                                     std::to_string(l->A) + ") in the batch; batch rejected, "
                                     "parameters unchanged");
@@ -954,6 +974,7 @@ extern "C" int fi_learner_load_state(fi_learner* l, const void* src, size_t byte
 static int ensure_comm_stream(fi_learner* l) {
     if (!l->comm_stream) FI_HIP_CHECK(hipStreamCreateWithFlags(&l->comm_stream, hipStreamNonBlocking));
     if (!l->comm_done) FI_HIP_CHECK(hipEventCreateWithFlags(&l->comm_done, hipEventDisableTiming));
+    if (!l->bad_ready) FI_HIP_CHECK(hipEventCreateWithFlags(&l->bad_ready, hipEventDisableTiming));
     return FI_OK;
 }
 

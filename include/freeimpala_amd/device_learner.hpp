@@ -362,6 +362,9 @@ private:
         for (size_t g = 1; g < G; ++g) th.emplace_back(run, g);
         run(0);
         for (auto& t : th) t.join();
+        // A rejected batch (an out-of-range action in any shard) fails on EVERY shard: the
+        // reject counter is all-reduced with the gradient before the optimizer, so all
+        // replicas skip the update together and stay identical; one rejection is reported.
         for (size_t g = 0; g < G; ++g)
             if (rc[g] != FI_OK) return fail(p, "shard " + std::to_string(g) + ": " + why[g]);
         fi_step_stats sum = st[0];

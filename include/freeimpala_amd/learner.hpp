@@ -38,6 +38,7 @@
 #pragma once
 
 #include <atomic>
+#include <cstring>
 #include <cstdio>
 #include <filesystem>
 #include <fstream>
@@ -91,6 +92,10 @@ inline bool read_file(const std::string& path, std::vector<char>& out) {
     f.read(out.data(), (std::streamsize)out.size());
     return (bool)f;
 }
+struct ModelSnapshot {
+    uint64_t version;
+    std::vector<char> blob;
+};
 inline std::string state_path_for(const std::string& model_file) {
     std::filesystem::path p(model_file);
     p.replace_extension(".state");
@@ -146,9 +151,13 @@ public:
         checkpoint_threads_.clear();
         if (!final_saved_.exchange(true)) {
             log("info", "Performing final model save before exit");
-            // workers are joined: the device state can be read from this thread
-            for (size_t q = 0; q < num_players_; ++q) save_state_sidecars(q, total_iterations_);
-            model_manager_->saveAllModels(total_iterations_);
+            // workers are joined: the device state and the published model are read from this
+            // thread (learner.h:186-196 saveAllModels(T), written from the same snapshot)
+            for (size_t q = 0; q < num_players_; ++q) {
+                std::vector<char> st;
+                const bool have = save_state_sidecars(q, total_iterations_, &st);
+                write_checkpoint(q, total_iterations_, snapshot(q), have ? &st : nullptr);
+            }
         }
     }
 
@@ -175,6 +184,7 @@ public:
     DeviceLearner& device() { return *device_; }
     const LearnerConfig& config() const { return cfg_; }
     size_t learnerTimeMs() const { return train_time_ms_; }  // accepted; the device step replaces the sleep
+    bool workerFailed() const { return worker_failed_.load(); }  // a worker ended on a device failure
 
 private:
     void workerThread(size_t player_index) {
@@ -183,7 +193,9 @@ private:
             bool got = false;
             if constexpr (detail::has_read_batch_into<Buffer>::value) {
                 if (device_->shards(player_index) == 1) {
-                    got = step_zero_copy(player_index);
+                    const int r = step_zero_copy(player_index);
+                    if (r < 0) break;  // the staging buffer is unusable: this worker stops (logged)
+                    got = r > 0;
                 } else {  // --data-parallel: readBatch, then the shards step concurrently
                     auto batch = shared_buffers_[player_index]->readBatch(batch_size_);
                     got = !batch.empty();
@@ -205,16 +217,21 @@ private:
         }
     }
 
-    // readBatchInto the pinned staging buffer, then the step; returns whether a batch was read
-    bool step_zero_copy(size_t p) {
+    // readBatchInto the pinned staging buffer, then the step. Returns 1 when a batch was read
+    // (stepped or rejected), 0 when none was (draining / spurious wake-up), -1 when the staging
+    // buffer cannot be acquired: a device-side failure that retrying would only repeat, so the
+    // worker ends (logged once) instead of spinning on it.
+    int step_zero_copy(size_t p) {
         fi_learner* h = device_->handle(p);
         void* dst = nullptr;
         size_t stride = 0;
         if (fi_learner_acquire_staging(h, &dst, &stride) != FI_OK) {
-            log("error", std::string("acquire_staging: ") + fi_last_error());
-            return false;
+            log("error", "player " + std::to_string(p) + ": acquire_staging failed, worker stops: " +
+                             fi_last_error());
+            worker_failed_.store(true);
+            return -1;
         }
-        if (!shared_buffers_[p]->readBatchInto(batch_size_, static_cast<char*>(dst), stride)) return false;
+        if (!shared_buffers_[p]->readBatchInto(batch_size_, static_cast<char*>(dst), stride)) return 0;
         auto metrics = Metrics::getInstance();
         bool ok;
         {
@@ -224,7 +241,7 @@ private:
             if (ok) publish(p, true, &st);
         }
         if (!ok) rejected(p, fi_last_error());
-        return true;
+        return 1;
     }
 
     void rejected(size_t p, const std::string& why) {
@@ -300,12 +317,46 @@ private:
         detail::write_file_atomic(base + "latest.state", st);
     }
 
-    // learner.h:52-69: earlier checkpoint threads are joined, then a new one saves this
-    // player's model; the optimizer state is read here, on the worker thread that owns the
-    // device handle, and written by the checkpoint thread beside the model file
+    // The published model of player p (what actors see), copied under the Model's own lock.
+    // On the worker thread that owns the device handle it is exactly the device state the
+    // optimizer-state blob is read from, so the pair written below belongs to one iteration.
+    std::shared_ptr<const detail::ModelSnapshot> snapshot(size_t p) {
+        auto m = model_manager_->getModel(p)->createCopy();
+        return std::make_shared<const detail::ModelSnapshot>(detail::ModelSnapshot{m->getVersion(), m->getData()});
+    }
+
+    // <dir>/model_<p>_<iter>.bin and model_<p>_latest.bin in the reference file format
+    // (`u64 version || blob`, data_structures.h:105-110), plus the .state sidecars. Written
+    // here from the snapshot instead of through Manager::saveModel: the reference's saveModel
+    // re-creates the copy as a fresh Model before saving (data_structures.h:409-410), whose
+    // constructor fills it with rand() bytes, so its checkpoint files never hold the trained
+    // weights; and a saveModel on the checkpoint thread would read whatever version is current
+    // then, not the one the optimizer state belongs to.
+    void write_checkpoint(size_t p, uint64_t it, const std::shared_ptr<const detail::ModelSnapshot>& snap,
+                          const std::vector<char>* state) const {
+        std::vector<char> file(sizeof(uint64_t) + snap->blob.size());
+        std::memcpy(file.data(), &snap->version, sizeof(uint64_t));
+        std::memcpy(file.data() + sizeof(uint64_t), snap->blob.data(), snap->blob.size());
+        std::error_code ec;
+        std::filesystem::create_directories(checkpoint_location_, ec);
+        const std::string base = checkpoint_location_ + "/model_" + std::to_string(p) + "_";
+        if (!detail::write_file_atomic(base + std::to_string(it) + ".bin", file) ||
+            !detail::write_file_atomic(base + "latest.bin", file)) {
+            log("error", "Failed to save checkpoint for player " + std::to_string(p));
+            return;
+        }
+        log("info", "Saved checkpoint for player " + std::to_string(p) + " at iteration " + std::to_string(it) +
+                        " to " + base + std::to_string(it) + ".bin (version " + std::to_string(snap->version) + ")");
+        if (state) write_sidecars(p, it, *state);
+    }
+
+    // learner.h:52-69: earlier checkpoint threads are joined, then a new one writes this
+    // player's checkpoint. The model snapshot and the optimizer state are both taken here, on
+    // the worker thread, so the .bin and the .state of one checkpoint hold the same iteration.
     void checkpointModel(size_t p, uint64_t it) {
         auto st = std::make_shared<std::vector<char>>();
         const bool have = save_state_sidecars(p, it, st.get());
+        auto snap = snapshot(p);
         std::lock_guard<std::mutex> lk(checkpoint_mutex_);
         for (auto i = checkpoint_threads_.begin(); i != checkpoint_threads_.end();) {
             if (i->joinable()) {
@@ -315,10 +366,8 @@ private:
                 ++i;
             }
         }
-        checkpoint_threads_.emplace_back([this, p, it, st, have] {
-            model_manager_->saveModel(p, it);
-            if (have) write_sidecars(p, it, *st);
-        });
+        checkpoint_threads_.emplace_back(
+            [this, p, it, st, have, snap] { write_checkpoint(p, it, snap, have ? st.get() : nullptr); });
     }
 
     static void log(const char* level, const std::string& m) {
@@ -333,7 +382,7 @@ private:
     std::vector<std::shared_ptr<Buffer>> shared_buffers_;
     std::shared_ptr<Manager> model_manager_;
     std::vector<std::thread> worker_threads_, checkpoint_threads_;
-    std::atomic<bool> should_stop_{false}, final_saved_{false};
+    std::atomic<bool> should_stop_{false}, final_saved_{false}, worker_failed_{false};
     std::mutex checkpoint_mutex_;
     std::vector<std::atomic<size_t>> iterations_;
 };

@@ -50,7 +50,8 @@ namespace mpi {
 
 struct EndpointStats {
     uint64_t trajectories = 0, trajectory_bytes = 0, version_requests = 0, weights_replies = 0,
-             weights_bytes = 0, bad_messages = 0, dropped_entries = 0;
+             weights_bytes = 0, bad_messages = 0, dropped_entries = 0,
+             late_messages = 0;  // completed receives found in the slots after the last terminate
     double seconds = 0.0;  // from the first slot posted to the last actor's TAG_TERMINATE
 };
 
@@ -98,11 +99,32 @@ public:
             post(bufs[idx], reqs[idx]);
         }
         const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        for (auto& r : reqs)
-            if (r != MPI_REQUEST_NULL) {
+        // Drain the posted slots. MPI_Waitany hands back an arbitrary completed request, so
+        // the last TAG_TERMINATE may have been picked while other slots already held
+        // trajectories that arrived before it: a slot whose receive completed (or completes
+        // while being cancelled) is enqueued like any other message, never thrown away.
+        for (int i = 0; i < n_slots_; ++i) {
+            MPI_Request& r = reqs[i];
+            if (r == MPI_REQUEST_NULL) continue;
+            MPI_Status st;
+            int flag = 0;
+            MPI_Test(&r, &flag, &st);
+            if (!flag) {
                 MPI_Cancel(&r);
-                MPI_Wait(&r, MPI_STATUS_IGNORE);
+                MPI_Wait(&r, &st);
+                int cancelled = 0;
+                MPI_Test_cancelled(&st, &cancelled);
+                if (cancelled) continue;
             }
+            if (st.MPI_TAG == TAG_TERMINATE) {  // a surplus terminate: counted, not fatal
+                bump(&EndpointStats::late_messages);
+                continue;
+            }
+            int n = 0;
+            MPI_Get_count(&st, MPI_BYTE, &n);
+            bump(&EndpointStats::late_messages);
+            enqueue(Msg{st.MPI_TAG, st.MPI_SOURCE, (size_t)n, std::move(bufs[i])});
+        }
         {
             std::lock_guard<std::mutex> lk(qmu_);
             stopping_ = true;

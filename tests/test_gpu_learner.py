@@ -364,3 +364,42 @@ def test_out_of_range_action_rejects_batch(orc):
     r = R.step(pk(good))
     assert s["version"] == r["version"] == 2
     np.testing.assert_array_equal(L.get_params(), R.get_params())
+
+
+@pytest.mark.parametrize("attach", ["uid", "init_all"])
+def test_rejected_batch_under_comm_leaves_state_unchanged(orc, monkeypatch, attach):
+    """With a communicator attached the reject decision is all-reduced (a one-int
+    ncclAllReduce(sum) of the bad-action counter after the last gradient bucket) and the
+    optimizer reads the reduced flag, so every replica skips a batch that any shard rejects.
+    On one GPU (FI_COMM_SINGLE one-rank communicator, both attach forms): a bad batch through
+    the in-step all-reduce path raises FI_ERR_INVALID and leaves parameters, both Adam moments
+    and the version bit-unchanged; the next good batch then matches a handle without a
+    communicator bit for bit."""
+    from freeimpala_amd._abi import FiError
+    from freeimpala_amd.learner import DeviceLearner, pack_records
+    monkeypatch.setenv("FI_COMM_SINGLE", "1")
+    T, B = 4, 32
+    good = orc.synth_batch(43, T=T, B=B, A=18, D=128)
+    bad = {k: (None if v is None else v.copy()) for k, v in good.items()}
+    bad["actions"][3, 31] = 18
+    pk = lambda b: pack_records(b["obs"], b["mu"], b["actions"], b["rewards"], b["discounts"],
+                                entry_size=T + 1)
+    L, R = mk(T=T, B=B, seed=6, optimizer="adam"), mk(T=T, B=B, seed=6, optimizer="adam")
+    if attach == "uid":
+        L.attach_comm(DeviceLearner.comm_unique_id(), 0, 1)
+    else:
+        DeviceLearner.comm_init_all([L])
+    L.step(pk(good))
+    R.step(pk(good))
+    p1, m1, v1 = L.get_params(), L.tensor("adam_m"), L.tensor("adam_v")
+    with pytest.raises(FiError, match="outside"):
+        L.step(pk(bad))
+    np.testing.assert_array_equal(L.get_params(), p1)
+    np.testing.assert_array_equal(L.tensor("adam_m"), m1)
+    np.testing.assert_array_equal(L.tensor("adam_v"), v1)
+    assert L.comm_info()["buckets_last_step"] == 3
+    s, r = L.step(pk(good)), R.step(pk(good))
+    assert s["version"] == r["version"] == 2
+    np.testing.assert_array_equal(L.get_params(), R.get_params())
+    L.close()
+    R.close()

@@ -93,12 +93,13 @@ int run_learner(int world, const Params& P, const LearnerConfig& lc) {
     char buf[768];
     std::snprintf(buf, sizeof buf,
                   "{\"actors\": %d, \"trajectories\": %llu, \"trajectory_bytes\": %llu, \"version_requests\": %llu, "
-                  "\"weights_replies\": %llu, \"weights_bytes\": %llu, \"bad_messages\": %llu, "
+                  "\"weights_replies\": %llu, \"weights_bytes\": %llu, \"bad_messages\": %llu, \"late_messages\": %llu, "
                   "\"receive_seconds\": %.4f, \"wall_seconds\": %.4f, \"e2e_env_steps_per_s\": %.1f, "
                   "\"receive_GBps\": %.4f}",
                   world - 1, (unsigned long long)es.trajectories, (unsigned long long)es.trajectory_bytes,
                   (unsigned long long)es.version_requests, (unsigned long long)es.weights_replies,
-                  (unsigned long long)es.weights_bytes, (unsigned long long)es.bad_messages, es.seconds, wall,
+                  (unsigned long long)es.weights_bytes, (unsigned long long)es.bad_messages,
+                  (unsigned long long)es.late_messages, es.seconds, wall,
                   wall > 0 ? env_steps / wall : 0.0, es.seconds > 0 ? es.trajectory_bytes / es.seconds / 1e9 : 0.0);
     report(P, "{\"learner_iterations\": " + iterations_json(*learner, P.num_players) +
                   ", \"expected_iterations\": " + std::to_string(learner_iterations) + ", \"param_bytes\": " +
