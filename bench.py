@@ -219,20 +219,12 @@ def main():
     st = L.step_resident(stats=True)
 
     work = kernel_work(args.arch, T, B, A)
-    # HBM bytes per launch from the committed rocprofv3 PMC passes (scripts/pmc_pass.sh,
-    # corrected as MI355X_MICROARCH.md prescribes); only valid for the same T/B/A config
-    traffic = {}
-    tpath = os.path.join(ROOT, "profiles", f"r01_pmc_traffic_{args.arch}.json")
-    if os.path.exists(tpath) and (T, B, A) == (100, 4096, 18):
-        with open(tpath) as fh:
-            traffic = {k: v["hbm_bytes_per_launch"] for k, v in json.load(fh).items() if not k.startswith("_")}
-    # MFMA utilisation and effective clock per kernel from the committed counter pass
-    # (scripts/pmc_mfma.sh), same config only
-    mfma = {}
-    mpath = os.path.join(ROOT, "profiles", f"r01_pmc_mfma_{args.arch}.json")
-    if os.path.exists(mpath) and (T, B, A) == (100, 4096, 18):
-        with open(mpath) as fh:
-            mfma = {k: v for k, v in json.load(fh).items() if not k.startswith("_")}
+    # Counter fields from the committed rocprofv3 PMC summaries (scripts/pmc_pass.sh: HBM bytes
+    # per launch, corrected as MI355X_MICROARCH.md prescribes; scripts/pmc_mfma.sh: MFMA busy
+    # and clock), ONLY when a summary is stamped with the source hash of the tree this bench
+    # runs from (freeimpala_amd/build_info.py) and the same T/B/A: counters of another build
+    # are refused and the fields stay null (counters_build says which).
+    traffic, mfma, counters_build = load_counters(args.arch, (T, B, A))
     per_step = {k: v["ms"] * v["count"] / max(1, args.profile_steps) for k, v in kt.items()}
     dominant = max(per_step, key=per_step.get) if per_step else None
     dtype = "bf16" if args.arch == "atari" else "fp32"
@@ -286,6 +278,7 @@ def main():
         "final_loss": st["total_loss"], "grad_norm": st["grad_norm"],
         # RCCL's own view of the data-parallel communicator (ncclCommCount / ncclCommUserRank)
         "comm": L.comm_info(),
+        "counters_build": counters_build,
     }
     if rank == 0 and N == 1 and not args.no_cpu_baseline:
         # every core this process may use: the box's OMP_NUM_THREADS share when set (16 per GPU
@@ -293,6 +286,11 @@ def main():
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or host_cpu_info()["affinity_cpus"] or 1
         try:
             result["cpu_baseline"] = cpu_baseline(args.arch, T, A, args.cpu_seconds, threads)
+            result["cpu_baseline"]["threads_basis"] = (
+                "OMP_NUM_THREADS from the environment: the pool gives one GPU's job a 16-CPU share and "
+                "sets OMP_NUM_THREADS=16 (nproc / the affinity mask count the whole host, shared with "
+                "the node's other GPUs)" if os.environ.get("OMP_NUM_THREADS") else
+                "the process affinity mask (no OMP_NUM_THREADS set)")
             result["speedup_vs_cpu"] = round(value / result["cpu_baseline"]["value"], 1)
         except Exception as e:  # the baseline is reported, never blocks the GPU number
             result["cpu_baseline"] = {"error": repr(e)}
@@ -301,6 +299,34 @@ def main():
     L.close()
     if ws > 1:
         dist.destroy_process_group()
+
+
+def load_counters(arch, tba):
+    """(traffic, mfma, info) from the newest profiles/*pmc_{traffic,mfma}_<arch>*.json whose
+    _build.source_hash matches this tree; empty dicts when none does."""
+    import glob
+    from freeimpala_amd.build_info import source_hash
+    h = source_hash()
+    info = {"source_hash": h, "traffic_file": None, "mfma_file": None}
+    if tba != (100, 4096, 18):
+        return {}, {}, dict(info, note="counter passes exist for T=100 B=4096 A=18 only")
+
+    def newest(kind):
+        for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc_{kind}_{arch}*.json")), reverse=True):
+            try:
+                with open(f) as fh:
+                    d = json.load(fh)
+            except (OSError, ValueError):
+                continue
+            if d.get("_build", {}).get("source_hash") == h:
+                return os.path.relpath(f, ROOT), {k: v for k, v in d.items() if not k.startswith("_")}
+        return None, {}
+
+    info["traffic_file"], tr = newest("traffic")
+    info["mfma_file"], mf = newest("mfma")
+    if not info["traffic_file"] and not info["mfma_file"]:
+        info["note"] = "no counter pass stamped with this source hash: traffic / mfma_util_pmc null"
+    return {k: v["hbm_bytes_per_launch"] for k, v in tr.items()}, mf, info
 
 
 def kernel_times(L):

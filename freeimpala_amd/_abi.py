@@ -77,6 +77,7 @@ SIGNATURES = {
     "fi_comm_init_all": ([_P, C.c_int], C.c_int),
     "fi_learner_comm_info": ([_P, _P, _P, _P], C.c_int),
     "fi_learner_tensor": ([_P, C.c_char_p, C.POINTER(_P), C.POINTER(C.c_size_t)], C.c_int),
+    "fi_learner_read_tensor": ([_P, C.c_char_p, _P, C.c_size_t], C.c_int),
     "fi_learner_set_profiling": ([_P, C.c_int], C.c_int),
     "fi_learner_phase_times": ([_P, C.POINTER(C.c_float), C.c_int, C.POINTER(C.c_int)], C.c_int),
     "fi_learner_kernel_times": ([_P, C.c_char_p, C.c_size_t, C.POINTER(C.c_float),

@@ -1,0 +1,43 @@
+"""Build identity of libfi_learner.so's sources, used to stamp counter passes.
+
+`source_hash()` is a sha256 over every file the library is built from (freeimpala_amd/csrc/*,
+include/fi_learner.h, include/fi_farmer.h, the Makefile), so a rocprofv3 PMC summary under
+profiles/ can be matched to the exact kernels a bench line timed: bench.py attaches counter
+fields (HBM traffic, MFMA utilisation) only from a summary whose `_build.source_hash` equals the
+hash of the tree it runs from, and reports them as null otherwise.
+"""
+from __future__ import annotations
+
+import glob
+import hashlib
+import os
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def source_files():
+    files = sorted(glob.glob(os.path.join(ROOT, "freeimpala_amd", "csrc", "*")))
+    files += [os.path.join(ROOT, p) for p in ("include/fi_learner.h", "include/fi_farmer.h", "Makefile")]
+    return [f for f in files if os.path.isfile(f)]
+
+
+def source_hash() -> str:
+    h = hashlib.sha256()
+    for f in source_files():
+        h.update(os.path.relpath(f, ROOT).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    return h.hexdigest()[:16]
+
+
+def stamp(extra=None) -> dict:
+    """The `_build` object a counter summary carries."""
+    d = {"source_hash": source_hash()}
+    if extra:
+        d.update(extra)
+    return d
+
+
+if __name__ == "__main__":
+    print(source_hash())

@@ -1070,6 +1070,18 @@ extern "C" int fi_learner_comm_info(fi_learner* l, int* nranks, int* rank, int* 
 }
 
 // ------------------------------------------------------------------ introspection
+extern "C" int fi_learner_read_tensor(fi_learner* l, const char* name, void* dst, size_t bytes) {
+    FI_REQUIRE(l && name && dst, "read_tensor: null argument");
+    void* p = nullptr;
+    size_t have = 0;
+    FI_TRY(fi_learner_tensor(l, name, &p, &have));
+    FI_REQUIRE(bytes <= have, std::string("read_tensor: ") + name + " holds " + std::to_string(have) + " bytes");
+    FI_HIP_CHECK(hipSetDevice(l->dev));
+    FI_HIP_CHECK(hipStreamSynchronize(l->stream));
+    FI_HIP_CHECK(hipMemcpy(dst, p, bytes, hipMemcpyDeviceToHost));
+    return FI_OK;
+}
+
 extern "C" int fi_learner_tensor(fi_learner* l, const char* name, void** ptr, size_t* bytes) {
     FI_REQUIRE(l && name && ptr && bytes, "tensor: null argument");
     const size_t rows = l->rows, TB = l->TB, A = l->A;

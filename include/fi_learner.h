@@ -163,6 +163,10 @@ enum fi_phase {
     FI_PHASE_ALLREDUCE = 4, FI_PHASE_OPTIMIZER = 5, FI_PHASE_COUNT = 6
 };
 int fi_learner_tensor(fi_learner* l, const char* name, void** dev_ptr, size_t* bytes);
+/* fi_learner_read_tensor: waits for the handle's stream, then copies the first `bytes` bytes
+ * of a named tensor into host memory (for hosts that do not link HIP: verification dumps,
+ * e.g. the CLI's --dump-dir gradients). FI_ERR_INVALID when bytes exceeds the tensor.      */
+int fi_learner_read_tensor(fi_learner* l, const char* name, void* host_dst, size_t bytes);
 int fi_learner_set_profiling(fi_learner* l, int on);
 int fi_learner_phase_times(fi_learner* l, float* ms, int n, int* n_steps);
 int fi_learner_kernel_times(fi_learner* l, char* names_buf, size_t buflen, float* ms,

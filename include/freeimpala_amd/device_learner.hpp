@@ -333,6 +333,7 @@ public:
     }
 
     size_t param_bytes() const { return fi_learner_param_bytes(handles_[0]); }
+    size_t param_count() const { return fi_learner_param_count(handles_[0]); }
     size_t entry_bytes() const { return fi_learner_entry_bytes(handles_[0]); }
     size_t players() const { return handles_.size(); }
     const fi_step_stats& last_stats(size_t p) const { return stats_.at(p); }

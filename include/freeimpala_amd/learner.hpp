@@ -41,6 +41,7 @@
 #include <cstring>
 #include <cstdio>
 #include <filesystem>
+#include <functional>
 #include <fstream>
 #include <memory>
 #include <mutex>
@@ -175,13 +176,22 @@ public:
             ok = device_->step(player_index, batch);
             if (ok) publish(player_index, true);
         }
+        if (ok && observer_) observer_(player_index, device_->last_stats(player_index), device_->handle(player_index));
         if (!ok) rejected(player_index, device_->last_error(player_index));
         return ok;
     }
 
+    // Verification hook: called on player p's worker thread after every successful step with
+    // the step's statistics and the player's (first-shard) handle, before the next batch is
+    // read -- the handle's tensors (e.g. "grads") still hold that step's values. Set before
+    // start().
+    using StepObserver = std::function<void(size_t, const fi_step_stats&, fi_learner*)>;
+    void setStepObserver(StepObserver f) { observer_ = std::move(f); }
+
     // iterations completed by player p's worker
     size_t iterations(size_t p) const { return iterations_.at(p).load(); }
     DeviceLearner& device() { return *device_; }
+    size_t param_bytes() const { return device_->param_bytes(); }
     const LearnerConfig& config() const { return cfg_; }
     size_t learnerTimeMs() const { return train_time_ms_; }  // accepted; the device step replaces the sleep
     bool workerFailed() const { return worker_failed_.load(); }  // a worker ended on a device failure
@@ -234,12 +244,13 @@ private:
         if (!shared_buffers_[p]->readBatchInto(batch_size_, static_cast<char*>(dst), stride)) return 0;
         auto metrics = Metrics::getInstance();
         bool ok;
+        fi_step_stats st{};
         {
             auto timer = metrics->createTrainingTimer();
-            fi_step_stats st{};
             ok = fi_learner_step_staged(h, &st) == FI_OK;
             if (ok) publish(p, true, &st);
         }
+        if (ok && observer_) observer_(p, st, h);
         if (!ok) rejected(p, fi_last_error());
         return 1;
     }
@@ -385,6 +396,7 @@ private:
     std::atomic<bool> should_stop_{false}, final_saved_{false}, worker_failed_{false};
     std::mutex checkpoint_mutex_;
     std::vector<std::atomic<size_t>> iterations_;
+    StepObserver observer_;
 };
 
 // freeimpala_amd's own buffer / model store / metrics (replay.hpp, metrics.hpp)

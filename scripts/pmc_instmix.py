@@ -4,7 +4,11 @@ import collections
 import csv
 import glob
 import json
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from freeimpala_amd import build_info  # noqa: E402
 
 KERNELS = ["conv21_bwd_fr", "conv3_bwd_fr", "conv12_fwd_fr", "conv_fwd_fr<3>", "vtrace_lds_kernel",
            "heads_dgrad", "heads_wgrad"]
@@ -39,6 +43,7 @@ def main(outdir, dst):
             # util = busy / (SIMDs x GRBM_GUI_ACTIVE / 8 XCDs), as scripts/pmc_mfma.py
             out["mfma_util"] = round(m["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * m["GRBM_GUI_ACTIVE"] / 8), 4)
         res[k] = out
+    res["_build"] = build_info.stamp({"arch": os.environ.get("FI_BENCH_ARCH", "atari")})
     with open(dst, "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res, indent=1))

@@ -10,6 +10,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
 OUT=$ROOT/gpurun_out
 TAG=${TAG:-r02}
+export FI_BENCH_ARCH=${ARCH:-atari}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp

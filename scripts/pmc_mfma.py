@@ -14,8 +14,14 @@ import os
 import sys
 from collections import defaultdict
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from freeimpala_amd import build_info  # noqa: E402
+
 TAGS = {"conv21_bwd": "conv21_bwd_fr", "conv12_fwd": "conv12_fwd_fr", "conv3_bwd": "conv3_bwd_fr",
-        "conv3_fwd": "conv_fwd_fr<3>", "vtrace": "vtrace_lds_kernel", "fc (hipBLASLt)": "Cijk_"}
+        "conv3_fwd": "conv_fwd_fr<3>", "vtrace": "vtrace_lds_kernel", "fc_wgrad": "fc_tn_kernel",
+        "fc_nt (own fwd/dgrad)": "fc_nt_kernel", "fc (hipBLASLt)": "Cijk_",
+        # MLP (config #2 network): the dominant kernel of that line is the data gradient of layer 2
+        "mlp_dgrad_l2": "EpiMask", "mlp_heads_bwd": "heads_bwd_fused_f32", "mlp_fwd_heads": "EpiHeads"}
 
 
 def main():
@@ -47,6 +53,7 @@ def main():
             if t >= 0.3e-3:  # the GRBM clock estimate reads high on shorter dispatches
                 e["clock_mhz"] = round(a / 8 / t / 1e6, 1)
         res[tag] = e
+    res["_build"] = build_info.stamp({"arch": os.environ.get("FI_BENCH_ARCH", "atari")})
     res["_method"] = __doc__.strip().splitlines()[0] + " -- util = SQ_VALU_MFMA_BUSY_CYCLES / (1024 * GRBM_GUI_ACTIVE / 8)"
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)

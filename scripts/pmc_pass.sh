@@ -17,4 +17,4 @@ for C in FETCH_SIZE WRITE_SIZE; do
   rc=$?; echo "pmc $C rc=$rc"
   [ $rc -ne 0 ] && exit $rc
 done
-python3 "$ROOT/scripts/pmc_traffic.py" "$OUT/pmc_FETCH_SIZE_$TAG" "$OUT/pmc_WRITE_SIZE_$TAG" "$OUT/pmc_traffic_${ARCH}_$TAG.json"
+python3 "$ROOT/scripts/pmc_traffic.py" "$OUT/pmc_FETCH_SIZE_$TAG" "$OUT/pmc_WRITE_SIZE_$TAG" "$OUT/pmc_traffic_${ARCH}_$TAG.json" "$ARCH"

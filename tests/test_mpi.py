@@ -18,7 +18,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from test_dropin import CONFIG1, _make, _oracle_sgd_grad
+from test_dropin import CONFIG1, _make, assert_step_matches_oracle
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 MPIEXEC = shutil.which("mpiexec", path="/opt/conda/bin") or shutil.which("mpiexec")
@@ -78,13 +78,7 @@ def test_config5_shape_mpi_end_to_end_vs_oracle(orc, tmp_path):
     assert out["metrics"]["learner_model_updates"] == 4 and out["metrics"]["rejected_batches"] == 0
     p = np.fromfile(dump / "params_0_0.bin", np.float32)
     for k in range(4):
-        batch = np.fromfile(dump / f"batch_0_{k}.bin", np.uint8)
-        assert batch.size == B * (T + 1) * 1024
-        g, _ = _oracle_sgd_grad(orc, p, batch, T, B, A, D, H)
-        p1 = np.fromfile(dump / f"params_0_{k + 1}.bin", np.float32)
-        l2 = np.linalg.norm((p.astype(np.float64) - p1) / lr - g) / np.linalg.norm(g)
-        assert l2 < 2e-3, (k, l2)
-        p = p1
+        p = assert_step_matches_oracle(orc, dump, k, p, T, B, A, D, H, lr)
     latest = np.fromfile(ck / "model_0_latest.bin", np.uint8)
     assert int(latest[:8].view(np.uint64)[0]) == 4
     np.testing.assert_array_equal(latest[8:].view(np.float32), p)

@@ -18,6 +18,7 @@
 
 #include "freeimpala_amd/flags.hpp"
 #include "freeimpala_amd/learner.hpp"
+#include "freeimpala_amd/sim_learner.hpp"
 
 namespace fi_cli {
 
@@ -59,6 +60,37 @@ public:
 };
 
 using CliLearner = BasicLearner<DumpingBuffer, DumpingManager, MetricsTracker>;
+
+// --dump-dir: after every step of player p also write the step's loss statistics
+// (stats_<p>_<k>.json) and, per named tensor, <name>_<p>_<k>.bin: the gradient ("grads", fp32,
+// all-reduced, before clipping) and -- where the network has them (MLP) -- the hidden
+// activations and the V-trace output gradients ("h1", "h2", "dlogits", "dvalue"), so a test can
+// check every stage of each step against the CPU oracle directly
+inline void install_dump_observer(CliLearner& l, size_t players) {
+    if (g_dump_dir.empty()) return;
+    auto count = std::make_shared<std::vector<size_t>>(players, 0);
+    l.setStepObserver([count](size_t p, const fi_step_stats& st, fi_learner* h) {
+        const size_t k = (*count)[p]++;  // one worker thread per player
+        const std::string sfx = "_" + std::to_string(p) + "_" + std::to_string(k);
+        for (const char* name : {"grads", "h1", "h2", "dlogits", "dvalue"}) {
+            void* dev = nullptr;
+            size_t bytes = 0;
+            if (fi_learner_tensor(h, name, &dev, &bytes) != FI_OK || !dev || !bytes) continue;
+            std::vector<char> host(bytes);
+            if (fi_learner_read_tensor(h, name, host.data(), bytes) == FI_OK) dump(name + sfx + ".bin", host.data(), bytes);
+        }
+        char js[384];
+        const int n = std::snprintf(js, sizeof js,
+                                    "{\"pg_loss\": %.17g, \"baseline_loss\": %.17g, \"entropy_loss\": %.17g, "
+                                    "\"total_loss\": %.17g, \"grad_norm\": %.17g, \"version\": %llu}",
+                                    st.pg_loss, st.baseline_loss, st.entropy_loss, st.total_loss, st.grad_norm,
+                                    (unsigned long long)st.version);
+        dump("stats" + sfx + ".json", js, (size_t)n);
+    });
+}
+
+// --learner sim: the reference's placeholder step (sleep + random bytes, learner.h:32-49)
+using CliSimLearner = SimLearner<DumpingBuffer, DumpingManager, MetricsTracker>;
 
 struct Params {
     size_t num_players, total_iterations, entry_size, buffer_capacity, batch_size, learner_time,
@@ -217,7 +249,8 @@ inline void report(const Params& P, const std::string& line) {
     }
 }
 
-inline std::string iterations_json(const CliLearner& l, size_t players) {
+template <class L>
+std::string iterations_json(const L& l, size_t players) {
     std::string s = "[";
     for (size_t p = 0; p < players; ++p) s += (p ? ", " : "") + std::to_string(l.iterations(p));
     return s + "]";

@@ -73,27 +73,24 @@ private:
 
 }  // namespace
 
-int main(int argc, char** argv) {
-    ArgumentParser program("fi_freeimpala");
-    setup_parser(program, "Parallel consumer-producer system for game simulation (MI355X learner)", true);
-    Params P{};
-    LearnerConfig lc;
-    if (const int rc = parse(program, argc, argv, P, lc, true); rc >= 0) return rc;
-
+template <class L>
+int run(const Params& P, const LearnerConfig& lc, const std::string& kind) {
     auto metrics = MetricsTracker::getInstance();
     metrics->start();
     const size_t learner_iterations = (P.num_agents * P.total_iterations) / P.batch_size;  // main.cpp:179
-    std::unique_ptr<CliLearner> learner;
+    std::unique_ptr<L> learner;
     try {
-        learner = std::make_unique<CliLearner>(P.num_players, P.buffer_capacity, P.entry_size, P.batch_size,
-                                               P.learner_time, P.checkpoint_freq, P.checkpoint_location,
-                                               P.starting_model, learner_iterations, lc);
+        learner = std::make_unique<L>(P.num_players, P.buffer_capacity, P.entry_size, P.batch_size, P.learner_time,
+                                      P.checkpoint_freq, P.checkpoint_location, P.starting_model, learner_iterations,
+                                      lc);
     } catch (const std::exception& e) {
         std::cerr << "learner: " << e.what() << "\n";
         return 2;
     }
     auto bufs = learner->getSharedBuffers();
     for (size_t p = 0; p < bufs.size(); ++p) bufs[p]->setId(p);
+    if constexpr (std::is_same_v<L, CliLearner>) install_dump_observer(*learner, P.num_players);
+    const auto t0 = std::chrono::steady_clock::now();
     learner->start();
 
     std::vector<std::unique_ptr<SyntheticAgent>> agents;
@@ -112,12 +109,36 @@ int main(int argc, char** argv) {
         while (learner->iterations(p) < learner_iterations &&
                std::chrono::steady_clock::now() - t_wait < std::chrono::minutes(10))
             std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     learner->stop();
     std::this_thread::sleep_for(std::chrono::milliseconds(100));
     metrics->stop();
 
-    report(P, "{\"learner_iterations\": " + iterations_json(*learner, P.num_players) +
+    // learner env-steps/s over the whole run: T x M per learner iteration (the BASELINE metric's
+    // unit; sleep-bound with --learner sim, as the reference's own config #1 is)
+    size_t iters = 0;
+    for (size_t p = 0; p < P.num_players; ++p) iters += learner->iterations(p);
+    const double env_steps = (double)iters * (double)learner->config().seq_length * (double)P.batch_size;
+    char buf[160];
+    std::snprintf(buf, sizeof buf, ", \"wall_seconds\": %.4f, \"learner_env_steps_per_s\": %.1f", wall,
+                  wall > 0 ? env_steps / wall : 0.0);
+    report(P, "{\"learner\": \"" + kind + "\", \"learner_iterations\": " + iterations_json(*learner, P.num_players) +
                   ", \"expected_iterations\": " + std::to_string(learner_iterations) + ", \"param_bytes\": " +
-                  std::to_string(learner->device().param_bytes()) + ", \"metrics\": " + metrics->summaryJson() + "}");
+                  std::to_string(learner->param_bytes()) + buf + ", \"metrics\": " + metrics->summaryJson() + "}");
     return 0;
+}
+
+int main(int argc, char** argv) {
+    ArgumentParser program("fi_freeimpala");
+    setup_parser(program, "Parallel consumer-producer system for game simulation (MI355X learner)", true);
+    program.add_argument("--learner")
+        .help("device: the MI355X learner step; sim: the reference's placeholder step (sleep --learner-time, "
+              "then random model bytes; learner.h:32-49), no GPU")
+        .default_value(std::string("device"))
+        .choices("device", "sim");
+    Params P{};
+    LearnerConfig lc;
+    if (const int rc = parse(program, argc, argv, P, lc, true); rc >= 0) return rc;
+    const std::string kind = program.get<std::string>("--learner");
+    return kind == "sim" ? run<CliSimLearner>(P, lc, kind) : run<CliLearner>(P, lc, kind);
 }

@@ -71,6 +71,7 @@ int run_learner(int world, const Params& P, const LearnerConfig& lc) {
     }
     auto bufs = learner->getSharedBuffers();
     for (size_t p = 0; p < bufs.size(); ++p) bufs[p]->setId(p);
+    install_dump_observer(*learner, P.num_players);
     learner->start();
 
     const auto t0 = std::chrono::steady_clock::now();
