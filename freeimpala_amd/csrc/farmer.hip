@@ -4,17 +4,18 @@
 // 46-66, 99-125; cmd/libtorch_bench/main.cpp:14-42, 117-135), rebuilt for MI355X in fp32
 // (the reference's precision):
 //   input projection  XP[B*T][512] = z W_ih^T + (b_ih + b_hh)      one MFMA GEMM (gemm_f32.hip)
-//   recurrence        lstm_fwd_kernel: one workgroup per 8 batch rows walks t = 0..T-1; the
-//                     rows' h_{t-1} sits in LDS ([k][row], broadcast float4 reads), W_hh^T
-//                     streams from L1/L2 (coalesced rows of the transposed copy), c in
+//   recurrence        lstm_fwd_reg_kernel: one 512-thread workgroup per R = 1/2/4 batch rows
+//                     walks t = 0..T-1 with W_hh resident in registers (128 weights per
+//                     thread), the rows' h_{t-1} in LDS ([k][row], broadcast float4 reads), c in
 //                     registers; packed-fp32 FMAs; gates i, f, g, o in PyTorch order
 //   torso             cat(h_T, x) -> 5 x (Linear 512 + ReLU) -> Linear 512 -> 1 (MFMA GEMMs
 //                     with bias+ReLU epilogues; the last layer a per-row dot)
 //   criterion         mse / mae / huber mean + its gradient, one deterministic block
 //   backward          dense layers: weight-gradient GEMMs into split-K slabs reduced in a
-//                     fixed order, ReLU-masked data gradients; BPTT: lstm_bwd_kernel walks
-//                     t = T-1..0 per 8 rows (dc in registers, dgates to HBM and LDS, dh_{t-1} =
-//                     dgates W_hh from LDS-broadcast dgates x coalesced W_hh rows); W_ih / W_hh
+//                     fixed order, ReLU-masked data gradients; BPTT: lstm_bwd_reg_kernel walks
+//                     t = T-1..0 per R rows (W_hh in registers as four 128-row quarters, dc in
+//                     registers, dgates to HBM and LDS, dh_{t-1} = dgates W_hh as four quarter
+//                     sums from LDS-broadcast dgates); W_ih / W_hh
 //                     gradients = two GEMMs over all B*T rows; bias = column sums
 //   optimizer         torch.optim.Adam / AdamW / SGD update formulas (single-tensor forms) in fp32
 // Everything is deterministic (no float atomics). One HIP stream per handle.
@@ -33,7 +34,6 @@ namespace fi {
 namespace farmer {
 
 constexpr int IN = 162, H = 128, G = 4 * H, XD = 484, CAT = H + XD, DW = 512;
-constexpr int RB = 8;  // batch rows per recurrence workgroup
 
 struct Off {
     size_t wih, whh, bih, bhh, w[7], b[7], total;
@@ -58,160 +58,212 @@ typedef float f32x4v __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float sigm(float a) { return 1.0f / (1.0f + __expf(-a)); }
 
-// WT[k][n] = W_hh[n][k] (the recurrence reads rows of W_hh^T, coalesced across units);
-// bsum = b_ih + b_hh
-__global__ void lstm_prep_kernel(const float* __restrict__ whh, const float* __restrict__ bih,
-                                 const float* __restrict__ bhh, float* __restrict__ wt, float* __restrict__ bsum) {
+// bsum = b_ih + b_hh (folded into the input projection's epilogue)
+__global__ void lstm_prep_kernel(const float* __restrict__ bih, const float* __restrict__ bhh, float* __restrict__ bsum) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < G * H) {
-        const int n = i / H, k = i - n * H;
-        wt[(size_t)k * G + n] = whh[i];
-    }
     if (i < G) bsum[i] = bih[i] + bhh[i];
 }
 
-// Forward recurrence. Thread (u, rh): hidden unit u, rows 4rh..4rh+3 of the workgroup's 8;
-// 16 gate accumulators (i, f, g, o x 4 rows) as packed pairs. Stores, per (row, t): gates
-// (post-activation) [B*T][512], c [B*T][128], h_{t-1} [B*T][128] (the W_hh gradient's
-// operand); h_T into cat[:, 0:128].
-__global__ __launch_bounds__(256) void lstm_fwd_kernel(const float* __restrict__ xp, const float* __restrict__ wt,
-                                                       int B, int T, float* __restrict__ gates,
-                                                       float* __restrict__ cst, float* __restrict__ hprev,
-                                                       float* __restrict__ cat) {
-    __shared__ __attribute__((aligned(16))) float hT[H][RB];
-    const int u = threadIdx.x & (H - 1), rh = threadIdx.x >> 7;
-    const int b0 = blockIdx.x * RB + 4 * rh;
-    float c[4], h[4];
+// The recurrences keep W_hh in REGISTERS: one 512-thread workgroup per R batch rows, each
+// thread holding 128 of W_hh's 65,536 weights for the whole sequence (256 KB per workgroup:
+// half of a CU's register file), so no step re-reads W_hh from L1/L2 and the batch rows are
+// spread over up to 256 workgroups (B = 512 -> R = 2, one workgroup per CU). Per step the
+// rows' h (or dgates) sit in LDS as [k][R] and are read by wave-uniform broadcast
+// ds_read_b128; R rows are processed with packed fp32 FMAs. Two barriers per step.
+// Packed fp32 FMA with one weight broadcast to both halves: w holds two consecutive weights
+// (w[k], w[k+1]) as one VGPR pair; SEL picks which one multiplies both halves of h
+// (op_sel / op_sel_hi on src0), so the weights stay 128 registers and no pair is duplicated.
+template <int SEL>
+__device__ __forceinline__ f32x2 pk_fma_bw(f32x2 w, f32x2 h, f32x2 acc) {
+    if constexpr (SEL == 0)
+        asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[0,1,1]" : "+v"(acc) : "v"(w), "v"(h));
+    else
+        asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,0,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "v"(w), "v"(h));
+    return acc;
+}
+__device__ __forceinline__ f32x2 pk_fma2(f32x2 w, f32x2 h, f32x2 acc) {
+    return __builtin_elementwise_fma(w, h, acc);
+}
+// keeps the compiler from hoisting every LDS read of a fully unrolled k loop to its top (that
+// needs 128 more registers than the weights leave)
+#define FI_SCHED_FENCE() asm volatile("" ::: "memory")
+
+// acc[r] += sum_k w[k] v[k][r] over k = 0..127: w as 64 register pairs, v in LDS as [k][R]
+// (broadcast reads: every lane of a wave reads the same address)
+template <int R>
+__device__ __forceinline__ void lstm_matvec(const f32x2 (&w)[H / 2], const float* v, float (&acc)[R]) {
+    if constexpr (R == 1) {
+        f32x2 a0 = {acc[0], 0.f}, a1 = {0.f, 0.f};  // lanes: k even / k odd
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        c[j] = 0.f;
-        h[j] = 0.f;
-        hT[u][4 * rh + j] = 0.f;
+        for (int k = 0; k < H; k += 4) {
+            const f32x4v hv = *(const f32x4v*)&v[k];
+            a0 = pk_fma2(w[k / 2], f32x2{hv.x, hv.y}, a0);
+            a1 = pk_fma2(w[k / 2 + 1], f32x2{hv.z, hv.w}, a1);
+            if ((k & 31) == 28) FI_SCHED_FENCE();
+        }
+        const f32x2 a = a0 + a1;
+        acc[0] = a.x + a.y;
+    } else if constexpr (R == 2) {
+        f32x2 a0 = {acc[0], acc[1]}, a1 = {0.f, 0.f};  // rows 0, 1; chains over k even / odd
+#pragma unroll
+        for (int k = 0; k < H; k += 2) {
+            const f32x4v hv = *(const f32x4v*)&v[2 * k];  // v[k][0..1], v[k+1][0..1]
+            a0 = pk_fma_bw<0>(w[k / 2], f32x2{hv.x, hv.y}, a0);
+            a1 = pk_fma_bw<1>(w[k / 2], f32x2{hv.z, hv.w}, a1);
+            if ((k & 15) == 14) FI_SCHED_FENCE();
+        }
+        const f32x2 a = a0 + a1;
+        acc[0] = a.x;
+        acc[1] = a.y;
+    } else {
+        f32x2 a01 = {acc[0], acc[1]}, a23 = {acc[2], acc[3]};
+#pragma unroll
+        for (int k = 0; k < H; k += 2) {
+            const f32x4v h0 = *(const f32x4v*)&v[4 * k];  // v[k][0..3]
+            const f32x4v h1 = *(const f32x4v*)&v[4 * k + 4];
+            a01 = pk_fma_bw<0>(w[k / 2], f32x2{h0.x, h0.y}, a01);
+            a23 = pk_fma_bw<0>(w[k / 2], f32x2{h0.z, h0.w}, a23);
+            a01 = pk_fma_bw<1>(w[k / 2], f32x2{h1.x, h1.y}, a01);
+            a23 = pk_fma_bw<1>(w[k / 2], f32x2{h1.z, h1.w}, a23);
+            if ((k & 7) == 6) FI_SCHED_FENCE();
+        }
+        acc[0] = a01.x;
+        acc[1] = a01.y;
+        acc[2] = a23.x;
+        acc[3] = a23.y;
     }
+}
+
+// Forward. Thread n (0..511) owns gate column n: W_hh[n][0..127] in registers; per step
+//   pre[r][n] = xp[row r][t][n] + sum_k W_hh[n][k] h_{t-1}[r][k]
+// then the cell update runs on item threads (r, u) = (tid / 128, tid % 128), tid < 128 R, which
+// keep c in a register: gates i, f, g, o (PyTorch order) -> c, h; h goes to LDS for the next
+// step. Stores per (row, t): gates (post-activation) [B*T][512], c [B*T][128], h_{t-1}
+// [B*T][128] (the W_hh gradient's operand); h_T into cat[:, 0:128].
+template <int R>
+__global__ __launch_bounds__(512) void lstm_fwd_reg_kernel(const float* __restrict__ xp, const float* __restrict__ whh,
+                                                          int B, int T, float* __restrict__ gates,
+                                                          float* __restrict__ cst, float* __restrict__ hprev,
+                                                          float* __restrict__ cat) {
+    __shared__ __attribute__((aligned(16))) float hs[H * R];  // h_{t-1}, [k][r]
+    __shared__ __attribute__((aligned(16))) float gs[R * G];  // gate pre-activations, [r][n]
+    const int n = threadIdx.x;
+    const int b0 = blockIdx.x * R;
+    f32x2 w[H / 2];  // W_hh[n][k], k = 0..127, as register pairs
+    {
+        const f32x4v* src = (const f32x4v*)(whh + (size_t)n * H);
+#pragma unroll
+        for (int k4 = 0; k4 < H / 4; ++k4) {
+            const f32x4v v = src[k4];
+            w[2 * k4] = f32x2{v.x, v.y};
+            w[2 * k4 + 1] = f32x2{v.z, v.w};
+        }
+    }
+    const bool item = n < R * H;
+    const int ir = n / H, iu = n % H, irow = b0 + ir;
+    const bool ivalid = item && irow < B;
+    float c = 0.f, h = 0.f;
+    if (n < R * H) hs[iu * R + ir] = 0.f;
     __syncthreads();
     for (int t = 0; t < T; ++t) {
-        f32x2 acc[4][2];  // [gate][row pair]
+        float acc[R];
 #pragma unroll
-        for (int g = 0; g < 4; ++g)
+        for (int r = 0; r < R; ++r) acc[r] = b0 + r < B ? xp[((size_t)(b0 + r) * T + t) * G + n] : 0.f;
+        lstm_matvec<R>(w, hs, acc);
 #pragma unroll
-            for (int p = 0; p < 2; ++p) {
-                float v[2];
-#pragma unroll
-                for (int q = 0; q < 2; ++q) {
-                    const int row = b0 + 2 * p + q;
-                    v[q] = row < B ? xp[((size_t)row * T + t) * G + g * H + u] : 0.f;
-                }
-                acc[g][p] = f32x2{v[0], v[1]};
-            }
-        const float* wk = wt + u;
-#pragma unroll 4
-        for (int k = 0; k < H; ++k) {
-            const f32x4v hv = *(const f32x4v*)&hT[k][4 * rh];
-            const f32x2 h01 = {hv.x, hv.y}, h23 = {hv.z, hv.w};
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const float w = wk[(size_t)k * G + g * H];
-                const f32x2 w2 = {w, w};
-                acc[g][0] = __builtin_elementwise_fma(w2, h01, acc[g][0]);
-                acc[g][1] = __builtin_elementwise_fma(w2, h23, acc[g][1]);
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int p = j >> 1, q = j & 1;
-            const float ig = sigm(acc[0][p][q]), fg = sigm(acc[1][p][q]);
-            const float gg = tanhf(acc[2][p][q]), og = sigm(acc[3][p][q]);
-            const float hp = h[j];
-            c[j] = fg * c[j] + ig * gg;
-            h[j] = og * tanhf(c[j]);
-            const int row = b0 + j;
-            if (row < B) {
-                const size_t e = (size_t)row * T + t;
-                float* gr = gates + e * G + u;
+        for (int r = 0; r < R; ++r) gs[r * G + n] = acc[r];
+        __syncthreads();  // pre-activations visible; every thread is done reading hs for step t
+        if (item) {
+            const float* gp = gs + ir * G + iu;
+            const float ig = sigm(gp[0]), fg = sigm(gp[H]), gg = tanhf(gp[2 * H]), og = sigm(gp[3 * H]);
+            const float hp = h;
+            c = fg * c + ig * gg;
+            h = og * tanhf(c);
+            hs[iu * R + ir] = h;
+            if (ivalid) {
+                const size_t e = (size_t)irow * T + t;
+                float* gr = gates + e * G + iu;
                 gr[0] = ig;
                 gr[H] = fg;
                 gr[2 * H] = gg;
                 gr[3 * H] = og;
-                cst[e * H + u] = c[j];
-                hprev[e * H + u] = hp;
-                if (t == T - 1) cat[(size_t)row * CAT + u] = h[j];
+                cst[e * H + iu] = c;
+                hprev[e * H + iu] = hp;
+                if (t == T - 1) cat[(size_t)irow * CAT + iu] = h;
             }
         }
-        __syncthreads();  // every thread has read hT for step t
-#pragma unroll
-        for (int j = 0; j < 4; ++j) hT[u][4 * rh + j] = h[j];
-        __syncthreads();
+        __syncthreads();  // h_t visible for step t + 1; gs free again
     }
 }
 
-// Backward recurrence (BPTT). dh_T = dcat[:, 0:128]; per step t = T-1..0, thread (u, rh):
-//   do = dh tanh(c_t); dc += dh o (1 - tanh^2 c_t); di = dc g; dg = dc i; df = dc c_{t-1}
-//   pre-activation grads (i, f, g, o) -> dG[B*T][512] (HBM) and dGT[512][8] (LDS)
-//   dc <- dc f;  dh_{t-1}[row][u] = sum_n dG[row][n] W_hh[n][u]
-__global__ __launch_bounds__(256) void lstm_bwd_kernel(const float* __restrict__ gates, const float* __restrict__ cst,
-                                                       const float* __restrict__ whh, const float* __restrict__ dcat,
-                                                       int B, int T, float* __restrict__ dG) {
-    __shared__ __attribute__((aligned(16))) float dGT[G][RB];
-    const int u = threadIdx.x & (H - 1), rh = threadIdx.x >> 7;
-    const int b0 = blockIdx.x * RB + 4 * rh;
-    float dh[4], dc[4];
+// Backward recurrence (BPTT), same shape. Thread (q, u) = (tid / 128, tid % 128) holds
+// W_hh[128 q + j][u], j = 0..127, in registers. Per step t = T-1..0, item threads (r, u):
+//   dh = sum_q part[q][r][u] (dh_T = dcat[:, 0:128]); do = dh tanh(c_t);
+//   dc += dh o (1 - tanh^2 c_t); di = dc g; dg = dc i; df = dc c_{t-1}
+//   pre-activation grads (i, f, g, o) -> dG[B*T][512] (HBM) and dGs[512][R] (LDS); dc <- dc f
+// then every thread: part[q][r][u] = sum_j dGs[128 q + j][r] W_hh[128 q + j][u] (the four
+// quarter sums of dh_{t-1} = dgates W_hh, reduced by the item threads next step).
+template <int R>
+__global__ __launch_bounds__(512) void lstm_bwd_reg_kernel(const float* __restrict__ gates, const float* __restrict__ cst,
+                                                          const float* __restrict__ whh, const float* __restrict__ dcat,
+                                                          int B, int T, float* __restrict__ dG) {
+    __shared__ __attribute__((aligned(16))) float dGs[G * R];    // [n][r]
+    __shared__ __attribute__((aligned(16))) float ps[4 * R * H];  // [q][r][u]
+    const int tid = threadIdx.x, q = tid / H, u = tid % H;
+    const int b0 = blockIdx.x * R;
+    f32x2 w[H / 2];  // W_hh[128 q + j][u], j = 0..127, as register pairs
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int row = b0 + j;
-        dh[j] = row < B ? dcat[(size_t)row * CAT + u] : 0.f;
-        dc[j] = 0.f;
-    }
+    for (int j = 0; j < H; j += 2)
+        w[j / 2] = f32x2{whh[(size_t)(q * H + j) * H + u], whh[(size_t)(q * H + j + 1) * H + u]};
+    const bool item = tid < R * H;
+    const int ir = tid / H, irow = b0 + ir;  // item (ir, u)
+    const bool ivalid = item && irow < B;
+    float dh = ivalid ? dcat[(size_t)irow * CAT + u] : 0.f, dc = 0.f;
     for (int t = T - 1; t >= 0; --t) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int row = b0 + j;
+        if (item) {
+            if (t < T - 1) dh = (ps[(0 * R + ir) * H + u] + ps[(1 * R + ir) * H + u]) +
+                                (ps[(2 * R + ir) * H + u] + ps[(3 * R + ir) * H + u]);
             float dgi = 0.f, dgf = 0.f, dgg = 0.f, dgo = 0.f;
-            if (row < B) {
-                const size_t e = (size_t)row * T + t;
+            if (ivalid) {
+                const size_t e = (size_t)irow * T + t;
                 const float* gr = gates + e * G + u;
                 const float ig = gr[0], fg = gr[H], gg = gr[2 * H], og = gr[3 * H];
                 const float ct = cst[e * H + u];
                 const float cp = t > 0 ? cst[(e - 1) * H + u] : 0.f;
                 const float tc = tanhf(ct);
-                const float d_o = dh[j] * tc;
-                dc[j] += dh[j] * og * (1.f - tc * tc);
-                const float di = dc[j] * gg, dgv = dc[j] * ig, df = dc[j] * cp;
+                const float d_o = dh * tc;
+                dc += dh * og * (1.f - tc * tc);
+                const float di = dc * gg, dgv = dc * ig, df = dc * cp;
                 dgi = di * ig * (1.f - ig);
                 dgf = df * fg * (1.f - fg);
                 dgg = dgv * (1.f - gg * gg);
                 dgo = d_o * og * (1.f - og);
-                dc[j] *= fg;
+                dc *= fg;
                 float* dr = dG + e * G + u;
                 dr[0] = dgi;
                 dr[H] = dgf;
                 dr[2 * H] = dgg;
                 dr[3 * H] = dgo;
             }
-            dGT[u][4 * rh + j] = dgi;
-            dGT[H + u][4 * rh + j] = dgf;
-            dGT[2 * H + u][4 * rh + j] = dgg;
-            dGT[3 * H + u][4 * rh + j] = dgo;
+            dGs[u * R + ir] = dgi;
+            dGs[(H + u) * R + ir] = dgf;
+            dGs[(2 * H + u) * R + ir] = dgg;
+            dGs[(3 * H + u) * R + ir] = dgo;
         }
-        __syncthreads();
+        __syncthreads();  // dgates visible; the item threads are done reading ps
         if (t > 0) {
-            f32x2 a01 = {0.f, 0.f}, a23 = {0.f, 0.f};
-            const float* wc = whh + u;
-#pragma unroll 8
-            for (int n = 0; n < G; ++n) {
-                const f32x4v g4 = *(const f32x4v*)&dGT[n][4 * rh];
-                const float w = wc[(size_t)n * H];
-                const f32x2 w2 = {w, w};
-                a01 = __builtin_elementwise_fma(w2, f32x2{g4.x, g4.y}, a01);
-                a23 = __builtin_elementwise_fma(w2, f32x2{g4.z, g4.w}, a23);
-            }
-            dh[0] = a01.x;
-            dh[1] = a01.y;
-            dh[2] = a23.x;
-            dh[3] = a23.y;
+            const float* dq = dGs + (size_t)q * H * R;
+            float part[R] = {};
+            lstm_matvec<R>(w, dq, part);
+#pragma unroll
+            for (int r = 0; r < R; ++r) ps[(q * R + r) * H + u] = part[r];
         }
-        __syncthreads();  // dGT is rewritten next step
+        __syncthreads();  // partial sums visible; dGs free again
     }
 }
+
+// rows per recurrence workgroup: the fewest that keep the workgroup count within one per CU
+static int lstm_rows(int B) { return B <= 256 ? 1 : (B <= 512 ? 2 : 4); }
 
 // cat[b][128:612] = x[b]
 __global__ void cat_x_kernel(const float* __restrict__ x, int B, float* __restrict__ cat) {
@@ -324,7 +376,7 @@ struct fi_farmer {
     Off off;
     uint64_t step = 0;
     float *params = nullptr, *grads = nullptr, *m = nullptr, *v = nullptr;
-    float *wt = nullptr, *bsum = nullptr;
+    float *bsum = nullptr;
     float *z = nullptr, *x = nullptr, *y = nullptr;                   // resident input buffers
     float *xp = nullptr, *gates = nullptr, *cst = nullptr, *hprev = nullptr, *dG = nullptr;
     float *cat = nullptr, *act[6] = {}, *val = nullptr, *dval = nullptr, *dcat = nullptr;
@@ -333,6 +385,10 @@ struct fi_farmer {
     size_t slab_floats = 0;
     double* loss = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
+    hipEvent_t pe[4] = {};  // profiling: around lstm_fwd, around lstm_bwd
+    bool profiling = false;
+    double prof_fwd = 0.0, prof_bwd = 0.0;
+    int prof_steps = 0;
     std::vector<void*> allocs;
 };
 
@@ -366,11 +422,15 @@ static int forward(fi_farmer* f) {
     const int B = f->B, T = f->T;
     const Off& o = f->off;
     float* P = f->params;
-    hipLaunchKernelGGL(lstm_prep_kernel, dim3((G * H + 255) / 256), dim3(256), 0, s, P + o.whh, P + o.bih, P + o.bhh,
-                       f->wt, f->bsum);
+    hipLaunchKernelGGL(lstm_prep_kernel, dim3((G + 255) / 256), dim3(256), 0, s, P + o.bih, P + o.bhh, f->bsum);
     FI_TRY(f32_gemm_nt(f->z, IN, B * T, IN, P + o.wih, f->bsum, G, false, f->xp, s));
-    hipLaunchKernelGGL(lstm_fwd_kernel, dim3((B + RB - 1) / RB), dim3(256), 0, s, f->xp, f->wt, B, T, f->gates, f->cst,
-                       f->hprev, f->cat);
+    const int R = lstm_rows(B);
+    const dim3 grid((B + R - 1) / R), blk(512);
+    if (f->profiling) FI_HIP_CHECK(hipEventRecord(f->pe[0], s));
+    if (R == 1) hipLaunchKernelGGL(lstm_fwd_reg_kernel<1>, grid, blk, 0, s, f->xp, P + o.whh, B, T, f->gates, f->cst, f->hprev, f->cat);
+    else if (R == 2) hipLaunchKernelGGL(lstm_fwd_reg_kernel<2>, grid, blk, 0, s, f->xp, P + o.whh, B, T, f->gates, f->cst, f->hprev, f->cat);
+    else hipLaunchKernelGGL(lstm_fwd_reg_kernel<4>, grid, blk, 0, s, f->xp, P + o.whh, B, T, f->gates, f->cst, f->hprev, f->cat);
+    if (f->profiling) FI_HIP_CHECK(hipEventRecord(f->pe[1], s));
     hipLaunchKernelGGL(cat_x_kernel, dim3((B * XD + 255) / 256), dim3(256), 0, s, f->x, B, f->cat);
     const float* in = f->cat;
     int K = CAT;
@@ -406,8 +466,15 @@ static int backward(fi_farmer* f) {
             FI_TRY(f32_gemm_nn_dgrad(dcur, B, DW, P + o.w[1], CAT, nullptr, f->dcat, s));
         }
     }
-    hipLaunchKernelGGL(lstm_bwd_kernel, dim3((B + RB - 1) / RB), dim3(256), 0, s, f->gates, f->cst, P + o.whh, f->dcat,
-                       B, T, f->dG);
+    {
+        const int R = lstm_rows(B);
+        const dim3 grid((B + R - 1) / R), blk(512);
+        if (f->profiling) FI_HIP_CHECK(hipEventRecord(f->pe[2], s));
+        if (R == 1) hipLaunchKernelGGL(lstm_bwd_reg_kernel<1>, grid, blk, 0, s, f->gates, f->cst, P + o.whh, f->dcat, B, T, f->dG);
+        else if (R == 2) hipLaunchKernelGGL(lstm_bwd_reg_kernel<2>, grid, blk, 0, s, f->gates, f->cst, P + o.whh, f->dcat, B, T, f->dG);
+        else hipLaunchKernelGGL(lstm_bwd_reg_kernel<4>, grid, blk, 0, s, f->gates, f->cst, P + o.whh, f->dcat, B, T, f->dG);
+        if (f->profiling) FI_HIP_CHECK(hipEventRecord(f->pe[3], s));
+    }
     FI_TRY(wgrad(f, f->dG, B * T, G, f->z, IN, IN, Gd + o.wih, Gd + o.bih));
     FI_TRY(wgrad(f, f->dG, B * T, G, f->hprev, H, H, Gd + o.whh, nullptr));
     hipLaunchKernelGGL(copy_kernel, dim3((G + 255) / 256), dim3(256), 0, s, Gd + o.bih, Gd + o.bhh, G);
@@ -480,7 +547,7 @@ extern "C" int fi_farmer_create(const fi_farmer_config* cfg, fi_farmer** out) {
         if (rc == FI_OK) rc = falloc(f, p, n);
     };
     A(&f->params, P); A(&f->grads, P); A(&f->m, P); A(&f->v, P);
-    A(&f->wt, (size_t)G * H); A(&f->bsum, G);
+    A(&f->bsum, G);
     A(&f->z, BT * IN); A(&f->x, B * XD); A(&f->y, B);
     A(&f->xp, BT * G); A(&f->gates, BT * G); A(&f->cst, BT * H); A(&f->hprev, BT * H); A(&f->dG, BT * G);
     A(&f->cat, B * CAT); A(&f->dcat, B * CAT);
@@ -516,6 +583,8 @@ extern "C" void fi_farmer_destroy(fi_farmer* f) {
     for (void* p : f->allocs) hipFree(p);
     if (f->e0) hipEventDestroy(f->e0);
     if (f->e1) hipEventDestroy(f->e1);
+    for (hipEvent_t e : f->pe)
+        if (e) hipEventDestroy(e);
     if (f->stream) hipStreamDestroy(f->stream);
     delete f;
 }
@@ -558,6 +627,15 @@ extern "C" int fi_farmer_train_step(fi_farmer* f, const float* z, const float* x
     FI_TRY(backward(f));
     FI_TRY(optimize(f));
     if (out) FI_HIP_CHECK(hipEventRecord(f->e1, f->stream));
+    if (f->profiling) {
+        FI_HIP_CHECK(hipEventSynchronize(f->pe[3]));
+        float a = 0.f, b = 0.f;
+        FI_HIP_CHECK(hipEventElapsedTime(&a, f->pe[0], f->pe[1]));
+        FI_HIP_CHECK(hipEventElapsedTime(&b, f->pe[2], f->pe[3]));
+        f->prof_fwd += a;
+        f->prof_bwd += b;
+        f->prof_steps++;
+    }
     if (values) FI_HIP_CHECK(hipMemcpyAsync(values, f->val, (size_t)f->B * 4, hipMemcpyDeviceToHost, f->stream));
     if (out) {
         double l = 0.0;
@@ -603,3 +681,23 @@ extern "C" int fi_farmer_tensor(fi_farmer* f, const char* name, void** ptr, size
 }
 
 extern "C" void* fi_farmer_stream(fi_farmer* f) { return f ? (void*)f->stream : nullptr; }
+
+extern "C" int fi_farmer_set_profiling(fi_farmer* f, int on) {
+    FI_REQUIRE(f, "farmer_set_profiling: null handle");
+    FI_HIP_CHECK(hipSetDevice(f->dev));
+    for (hipEvent_t& e : f->pe)
+        if (!e) FI_HIP_CHECK(hipEventCreate(&e));
+    f->profiling = on != 0;
+    return FI_OK;
+}
+
+extern "C" int fi_farmer_recurrence_ms(fi_farmer* f, float* fwd_ms, float* bwd_ms, int* steps) {
+    FI_REQUIRE(f && fwd_ms && bwd_ms, "farmer_recurrence_ms: null argument");
+    const int n = f->prof_steps;
+    *fwd_ms = n ? (float)(f->prof_fwd / n) : 0.f;
+    *bwd_ms = n ? (float)(f->prof_bwd / n) : 0.f;
+    if (steps) *steps = n;
+    f->prof_fwd = f->prof_bwd = 0.0;
+    f->prof_steps = 0;
+    return FI_OK;
+}

@@ -506,6 +506,199 @@ __global__ __launch_bounds__(64 * VtLayout<A>::NW, VtLayout<A>::WPS) void vtrace
     block_reduce3((double)pg, (double)base, (double)ent, (double*)smem, a.part + (size_t)blockIdx.x * 3);
 }
 
+// ------------------------------------------------------------------------------------
+// Kernel 3 (vtrace_seq_kernel<A>, the default for T <= 128): one 256-thread workgroup owns
+// NB = 2 batch columns for the WHOLE sequence, so there is no chain of chunks inside a
+// workgroup -- the only serial dependency of V-trace (the scalar carry acc_{t+1}) is resolved
+// by one in-register scan plus one cross-wave combine. The two columns' pi and mu logits
+// (T rows x 144 B each, 28.8 KB at T = 100) arrive by LDS-DMA in one burst (1-KiB contiguous
+// LDS per wave instruction, 144-B contiguous global runs), the scalars straight into
+// registers; 32 KB of LDS per workgroup lets five workgroups share a CU (20 waves), so one
+// workgroup's burst overlaps four others' arithmetic and 2048 workgroups keep the DMA
+// engines busy through the whole launch.
+// Lane map: lane = j + 32 c, column c = lane >> 5, j = 0..31 the wave's rows in REVERSE time
+// (t = 32 w + 31 - j), so the reverse recurrence acc_t = d_t + g_t acc_{t+1} is a prefix
+// scan in lane order inside each 32-lane half: DPP row_shr:1/2/4/8 inside 16-lane rows, then
+// row_bcast:15 into the upper row (the classic gfx9 scan, affine operator), identity (0, 1)
+// shifted in at the edges. Wave totals cross waves through LDS (one barrier).
+// dlogits are written over the lane's own pi row in LDS and leave as 16-byte stores in the
+// global layout's 144-B runs. Algorithmic HBM traffic: 12A+28 bytes per (t,b), as kernel 1.
+// ------------------------------------------------------------------------------------
+template <int A>
+struct VtSeq {
+    static constexpr int NB = 2;                // batch columns per workgroup
+    static constexpr int NT = 256;              // threads: 4 waves x 32 rows x 2 columns
+    static constexpr int TMAX = NT / NB;        // 128 timesteps
+    static constexpr int ROWB = NB * A * 4;     // bytes per t-row of a logits tile (144 at A=18)
+    static constexpr int PPR = ROWB / 16;       // 16-B pieces per t-row
+    static_assert(A % 2 == 0 && ROWB % 16 == 0, "pieces");
+    // LDS: pi tile [T][ROWB] | mu tile [T][ROWB] | wave totals [4 waves][2 (d, g)][NB] | loss scratch
+    static size_t lds_bytes(int T) { return (size_t)2 * T * ROWB + 4 * 2 * NB * 4 + 4 * 3 * 8; }
+};
+
+// identity-filled DPP move of a float (lanes whose source is out of range get `idf`)
+template <int CTRL, int ROWMASK = 0xf>
+__device__ __forceinline__ float vt_dppf(float v, float idf) {
+    return __uint_as_float(__builtin_amdgcn_update_dpp(__float_as_uint(idf), __float_as_uint(v), CTRL, ROWMASK, 0xf, false));
+}
+// one Hillis-Steele step of the affine prefix composition (D, G) <- (D + G D', G G'),
+// (D', G') = the value CTRL moves in (identity (0, 1) where there is none)
+template <int CTRL, int ROWMASK = 0xf>
+__device__ __forceinline__ void vt_affine_step(float& D, float& G) {
+    const float pd = vt_dppf<CTRL, ROWMASK>(D, 0.f), pg = vt_dppf<CTRL, ROWMASK>(G, 1.f);
+    D = fmaf(G, pd, D);
+    G = G * pg;
+}
+
+template <int A>
+__global__ __launch_bounds__(256, 5) void vtrace_seq_kernel(VtArgs a) {
+    using L = VtSeq<A>;
+    extern __shared__ __attribute__((aligned(16))) char vsm[];
+    const int T = a.T, B = a.B;
+    const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
+    const int cb = xcd_remap(blockIdx.x, gridDim.x);
+    const int b0 = cb * L::NB;
+    const int j = lane & 31, c = lane >> 5;
+    const int t = 32 * w + 31 - j;
+    const bool valid = t < T;
+    const int b = b0 + c;
+    const int tt = valid ? t : T - 1;  // rows past T read a valid row, contribute identity
+    char* const pit = vsm;
+    char* const mut = vsm + (size_t)T * L::ROWB;
+    float* const tot = (float*)(vsm + (size_t)2 * T * L::ROWB);
+
+    // 1. the pi and mu tiles by LDS-DMA: piece q of a tile = row q / PPR, 16 B at (q % PPR) * 16
+    {
+        const uint32_t lbytes = (uint32_t)T * B * A * 4;
+        const fi_i32x4 rpi = make_rsrc(a.pi, lbytes), rmu = make_rsrc(a.mu, lbytes);
+        const int npieces = T * L::PPR;
+        const uint32_t lds_pi = lds_addr(pit), lds_mu = lds_addr(mut);
+        for (int i = w; 64 * i < npieces; i += 4) {
+            const int q = 64 * i + lane;
+            if (q < npieces) {
+                const int row = q / L::PPR, pc = q - row * L::PPR;
+                const uint32_t off = (uint32_t)((row * B + b0) * A * 4 + pc * 16);
+                blds16(rpi, off, lds_pi + 1024 * i);
+                blds16(rmu, off, lds_mu + 1024 * i);
+            }
+        }
+    }
+    // 2. the scalars straight into registers (overlapping the DMA)
+    const size_t e = (size_t)tt * B + b;
+    int at = a.act[e];
+    const float rw = a.rew[e], g = a.disc[e], v = a.val[e], vn = a.val[e + B];
+    if (tid < L::NB) a.dval[(size_t)T * B + b0 + tid] = 0.f;
+    if (valid && (unsigned)at >= (unsigned)A) atomicAdd(a.bad, 1);
+    at = at < 0 ? 0 : (at >= A ? A - 1 : at);
+    wait_vmcnt(0);
+    lds_barrier();
+
+    // 3. softmax statistics of the lane's own row (as kernel 1)
+    constexpr float L2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
+    float* const zpi = (float*)(pit + (size_t)tt * L::ROWB) + c * A;
+    const float* const zmu = (const float*)(mut + (size_t)tt * L::ROWB) + c * A;
+    f32x2 zp2[A / 2], zm2[A / 2];
+#pragma unroll
+    for (int i = 0; i < A / 2; ++i) {
+        zp2[i] = *(const f32x2*)(zpi + 2 * i);
+        zm2[i] = *(const f32x2*)(zmu + 2 * i);
+    }
+    const float zpa = zpi[at], zma = zmu[at];
+    float mx = vt_max3(zp2[0].x, zp2[0].y, zp2[0].y), mm = vt_max3(zm2[0].x, zm2[0].y, zm2[0].y);
+#pragma unroll
+    for (int i = 1; i < A / 2; ++i) {
+        mx = vt_max3(mx, zp2[i].x, zp2[i].y);
+        mm = vt_max3(mm, zm2[i].x, zm2[i].y);
+    }
+    const f32x2 nmx = {-mx * L2E, -mx * L2E}, nmm = {-mm * L2E, -mm * L2E};
+    f32x2 e2[A / 2];
+    f32x2 sp2 = {0.f, 0.f}, sm2 = {0.f, 0.f}, sz2 = {0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < A / 2; ++i) {
+        const f32x2 ap = zp2[i] * L2E + nmx;
+        const f32x2 am = zm2[i] * L2E + nmm;
+        e2[i] = f32x2{VT_EXP2(ap.x), VT_EXP2(ap.y)};
+        sp2 += e2[i];
+        sz2 += e2[i] * zp2[i];
+        sm2 += f32x2{VT_EXP2(am.x), VT_EXP2(am.y)};
+    }
+    const fi_vtrace_hparams hp = a.hp;
+    const float sp = sp2.x + sp2.y, sm = sm2.x + sm2.y;
+    const float lse = mx + VT_LOG2(sp) * LN2, lsem = mm + VT_LOG2(sm) * LN2;
+    const float inv = __builtin_amdgcn_rcpf(sp);
+    const float plogp = (sz2.x + sz2.y) * inv - lse;
+    const float lpa = zpa - lse, lma = zma - lsem;
+    const float ratio = VT_EXP(lpa - lma);
+    const float rho = fminf(hp.rho_bar, ratio);
+    const float cc = hp.lambda_ * fminf(hp.c_bar, ratio);
+    const float pgr = fminf(hp.pg_rho_bar, ratio);
+    const float d_own = valid ? rho * (rw + g * vn - v) : 0.f;
+    const float g_own = valid ? g * cc : 1.f;
+
+    // 4. prefix composition in lane order (= reverse time) inside each 32-lane column half
+    float D = d_own, G = g_own;
+    vt_affine_step<0x111>(D, G);          // row_shr:1
+    vt_affine_step<0x112>(D, G);          // row_shr:2
+    vt_affine_step<0x114>(D, G);          // row_shr:4
+    vt_affine_step<0x118>(D, G);          // row_shr:8
+    vt_affine_step<0x142, 0xa>(D, G);     // row_bcast:15 into rows 1 and 3 (lanes 16-31, 48-63)
+    // exclusive composition (the rows after t inside the wave): one lane up, identity at j = 0
+    float Dx = vt_dppf<0x138>(D, 0.f), Gx = vt_dppf<0x138>(G, 1.f);  // wave_shr:1
+    if (j == 0) {
+        Dx = 0.f;
+        Gx = 1.f;
+    }
+    if (j == 31) {  // the wave's total for column c
+        tot[(w * 2 + 0) * L::NB + c] = D;
+        tot[(w * 2 + 1) * L::NB + c] = G;
+    }
+    __syncthreads();
+    float x = 0.f;  // acc at t = 32 (w + 1): later waves composed onto the bootstrap acc_T = 0
+#pragma unroll
+    for (int w2 = 3; w2 >= 0; --w2)
+        if (w2 > w) x = tot[(w2 * 2 + 0) * L::NB + c] + tot[(w2 * 2 + 1) * L::NB + c] * x;
+    const float acc_nx = Dx + Gx * x;  // acc_{t+1}
+    const float acc = d_own + g_own * acc_nx;
+    const float vs_t = v + acc;
+    const float adv = pgr * (rw + g * (vn + acc_nx) - v);
+    const float dv = -hp.baseline_cost * acc;
+
+    // 5. dlogits over the lane's own pi row: dz_i = e_i (alpha + beta z_i) - adv [i = a_t]
+    {
+        const float ec = hp.entropy_cost;
+        const float al = inv * (adv - ec * (plogp + lse)), be = inv * ec;
+        const f32x2 al2 = {al, al};
+        if (valid) {
+#pragma unroll
+            for (int i = 0; i < A / 2; ++i) *(f32x2*)(zpi + 2 * i) = e2[i] * (zp2[i] * be + al2);
+            zpi[at] -= adv;
+        }
+    }
+    if (valid) {
+        VT_ST(vs_t, a.vs + e);
+        VT_ST(adv, a.adv + e);
+        VT_ST(dv, a.dval + e);
+    }
+    float pg = valid ? -adv * lpa : 0.f, base = valid ? 0.5f * acc * acc : 0.f, ent = valid ? plogp : 0.f;
+    lds_barrier();  // dlogits rows complete
+
+    // 6. the dlogits tile out in the global layout (144-B runs), 16 B per lane
+    {
+        const int npieces = T * L::PPR;
+        for (int i = w; 64 * i < npieces; i += 4) {
+            const int q = 64 * i + lane;
+            if (q < npieces) {
+                const int row = q / L::PPR, pc = q - row * L::PPR;
+                const f32x4 d4 = *(const f32x4*)(pit + 16 * q);
+                VT_ST(d4, (f32x4*)(a.dlog + (size_t)(row * B + b0) * A) + pc);
+            }
+        }
+    }
+    // per-workgroup loss partials (summed in a fixed order later, as kernel 1)
+    block_reduce3((double)pg, (double)base, (double)ent, (double*)(tot + 4 * 2 * L::NB),
+                  a.part + (size_t)blockIdx.x * 3);
+}
+
 __global__ __launch_bounds__(256) void vtrace_finalize_kernel(const double* __restrict__ part,
                                                               int nblk, double* losses,
                                                               const int* bad) {
@@ -525,7 +718,7 @@ __global__ __launch_bounds__(256) void vtrace_finalize_kernel(const double* __re
 // ------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------
-static size_t vt_nblk_max(int B) { return (size_t)std::max((B + 7) / 8, (B + 255) / 256); }
+static size_t vt_nblk_max(int B) { return (size_t)std::max((B + 1) / 2, (B + 255) / 256); }
 
 // workspace: [sink floats][loss partials, 256-B padded][int bad-action counter, 256 B]
 static size_t vt_part_bytes(int B) { return (vt_nblk_max(B) * 3 * sizeof(double) + 255) & ~(size_t)255; }
@@ -541,6 +734,10 @@ static int* vt_bad_counter(void* ws, int B) {
 template <int A>
 static void launch_lds(const VtArgs& a, int nblk, hipStream_t s) {
     hipLaunchKernelGGL(vtrace_lds_kernel<A>, dim3(nblk), dim3(64 * VtLayout<A>::NW), 0, s, a);
+}
+template <int A>
+static void launch_seq(const VtArgs& a, int nblk, hipStream_t s) {
+    hipLaunchKernelGGL(vtrace_seq_kernel<A>, dim3(nblk), dim3(VtSeq<A>::NT), VtSeq<A>::lds_bytes(a.T), s, a);
 }
 
 static bool lds_supported(int A, int B) { return B % 8 == 0 && A % 2 == 0 && A >= 2 && A <= 20; }
@@ -569,6 +766,31 @@ int vtrace_launch(int variant, int T, int B, int A, const float* pi, const float
     // the LDS kernel's buffer descriptors and DMA offsets are 32-bit: T*B*A*4 must stay
     // below 2^31 bytes (else the column kernel, 64-bit indexing, runs)
     const bool fits32 = (size_t)T * B * A * sizeof(float) < ((size_t)1 << 31);
+    // variant 3 (whole-sequence workgroups) is the default where it applies: T <= 128
+    const bool seq_ok = lds_supported(A, B) && fits32 && T <= 128 && B % 2 == 0;
+    FI_REQUIRE(!(variant == 3 && !seq_ok), "vtrace: sequence kernel needs T<=128, B%8==0, even A<=20");
+    if (variant == 3 || (variant == 0 && seq_ok)) {
+        FI_REQUIRE(vs && adv, "vtrace: sequence kernel writes vs and pg_adv (non-null)");
+        FI_REQUIRE(((uintptr_t)pi | (uintptr_t)mu | (uintptr_t)dlog) % 16 == 0, "vtrace: needs 16-byte aligned logits");
+        const int nblk = B / 2;
+        switch (A) {
+            case 2: launch_seq<2>(a, nblk, stream); break;
+            case 4: launch_seq<4>(a, nblk, stream); break;
+            case 6: launch_seq<6>(a, nblk, stream); break;
+            case 8: launch_seq<8>(a, nblk, stream); break;
+            case 10: launch_seq<10>(a, nblk, stream); break;
+            case 12: launch_seq<12>(a, nblk, stream); break;
+            case 14: launch_seq<14>(a, nblk, stream); break;
+            case 16: launch_seq<16>(a, nblk, stream); break;
+            case 18: launch_seq<18>(a, nblk, stream); break;
+            case 20: launch_seq<20>(a, nblk, stream); break;
+            default: return fail(FI_ERR_UNSUPPORTED, "vtrace: A not instantiated");
+        }
+        FI_HIP_CHECK(hipGetLastError());
+        if (nblk_out) *nblk_out = nblk;
+        if (finalize) return vtrace_finalize_launch(ws, nblk, losses, stream, a.bad);
+        return FI_OK;
+    }
     bool use_lds = variant == 1 || (variant == 0 && lds_supported(A, B) && fits32);
     FI_REQUIRE(!(variant == 1 && !lds_supported(A, B)), "vtrace: LDS kernel needs B%8==0, even A<=20");
     FI_REQUIRE(!(variant == 1 && !fits32), "vtrace: LDS kernel needs T*B*A*4 < 2^31 bytes");

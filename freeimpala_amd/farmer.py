@@ -51,6 +51,8 @@ SIGNATURES = {  # every symbol include/fi_farmer.h declares
     "fi_farmer_forward": ([_P, _P, _P, C.c_int, _P], C.c_int),
     "fi_farmer_tensor": ([_P, C.c_char_p, C.POINTER(_P), C.POINTER(C.c_size_t)], C.c_int),
     "fi_farmer_stream": ([_P], _P),
+    "fi_farmer_set_profiling": ([_P, C.c_int], C.c_int),
+    "fi_farmer_recurrence_ms": ([_P, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_int)], C.c_int),
 }
 _bound = None
 
@@ -181,6 +183,17 @@ class FarmerLstmModel:
         if stats:
             self.last_step_ms = st.step_ms
         return st.loss if stats else None
+
+    def recurrence_ms(self, steps: int = 5):
+        """Mean device ms of the two recurrence kernels (forward LSTM, BPTT) over `steps`
+        resident train steps, from HIP events around each launch (bench roofline)."""
+        _abi.check(lib().fi_farmer_set_profiling(self._h, 1), "fi_farmer_set_profiling")
+        for _ in range(steps):
+            self.train_step_resident(stats=False)
+        f, b, n = C.c_float(), C.c_float(), C.c_int()
+        _abi.check(lib().fi_farmer_recurrence_ms(self._h, C.byref(f), C.byref(b), C.byref(n)), "fi_farmer_recurrence_ms")
+        _abi.check(lib().fi_farmer_set_profiling(self._h, 0), "fi_farmer_set_profiling")
+        return f.value, b.value
 
     def upload_inputs(self, z, x, targets) -> None:
         for name, a in (("z", z), ("x", x), ("targets", targets)):

@@ -73,6 +73,11 @@ int fi_farmer_forward(fi_farmer* f, const float* z, const float* x, int inputs_o
  * "targets" (the handle's resident input buffers), "gates", "h_last" */
 int fi_farmer_tensor(fi_farmer* f, const char* name, void** dev_ptr, size_t* bytes);
 void* fi_farmer_stream(fi_farmer* f);
+/* Profiling (bench / roofline): with profiling on, every later train step records HIP events
+ * around the two recurrence kernels; fi_farmer_recurrence_ms returns their mean device ms
+ * per step so far (forward LSTM, BPTT) and the step count, and resets the sums.          */
+int fi_farmer_set_profiling(fi_farmer* f, int on);
+int fi_farmer_recurrence_ms(fi_farmer* f, float* fwd_ms, float* bwd_ms, int* steps);
 
 #ifdef __cplusplus
 }

@@ -45,11 +45,21 @@ def main():
         hip.synchronize()
         dt = (time.perf_counter() - t0) / args.steps
         st_loss = M.train_step_resident(stats=True)  # + the device time of one step (HIP events)
+        fwd_ms, bwd_ms = M.recurrence_ms(5)
+        # recurrence rooflines: fp32 VALU (packed FMAs; 157.3 TF/s dense fp32 = the MFMA fp32 rate);
+        # algorithmic work = the h W_hh^T / dgates W_hh matvecs, 2 B T H 4H flops per kernel
+        fl = 2.0 * B * T * 128 * 512
+        roof = {}
+        for nm, ms in (("lstm_fwd", fwd_ms), ("lstm_bwd", bwd_ms)):
+            ach = fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
+            roof[nm] = {"launch_ms": round(ms, 5), "bound": "fp32", "algorithmic_flops": fl,
+                        "achieved": round(ach, 2), "peak": 157.3, "unit": "TFLOP/s", "frac": round(ach / 157.3, 4)}
         res = {"metric": "FarmerLstm train step samples/s (gpu_benchmark.py throughput)", "B": B, "T": T,
                "loss": args.loss, "optimizer": args.optimizer, "value": round(B / dt, 1), "unit": "samples/s",
                "ms_per_step": round(dt * 1e3, 4), "device_ms_one_step": round(M.last_step_ms, 4),
                "steps": args.steps, "dtype": "fp32",
-               "final_loss": st_loss, "data": "synthetic N(0,1) (numpy seed 2), resident in HBM"}
+               "final_loss": st_loss, "data": "synthetic N(0,1) (numpy seed 2), resident in HBM",
+               "roofline": roof}
         M.close()
         if not args.no_cpu:
             import torch

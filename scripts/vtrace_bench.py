@@ -22,6 +22,9 @@ def main():
     ap.add_argument("--B", type=int, default=4096)
     ap.add_argument("--A", type=int, default=18)
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--variant", type=int, action="append", default=[],
+                    help="kernel variant(s) to time (0 auto, 1 chunked LDS, 2 column, 3 whole-sequence)")
+    ap.add_argument("--sets", type=int, default=1, help="rotate over this many disjoint input/output sets (6: cold)")
     ap.add_argument("--stamps", action="store_true",
                     help="libs built with -DFI_VT_STAMPS: print per-phase timing of wave 0")
     args = ap.parse_args()
@@ -35,12 +38,15 @@ def main():
     rew = rng.integers(-1, 2, (T, B)).astype(np.float32)
     disc = (0.99 * (rng.random((T, B)) > 0.01)).astype(np.float32)
     val = rng.standard_normal((T + 1, B), dtype=np.float32)
-    bufs = [hip.DeviceBuffer.from_array(x) for x in (pi, mu, act, rew, disc, val)]
-    outs = [hip.DeviceBuffer(n) for n in (T * B * 4, T * B * 4, T * B * A * 4, (T + 1) * B * 4, 24)]
+    nsets = max(1, args.sets)
+    bufs = [[hip.DeviceBuffer.from_array(x) for x in (pi, mu, act, rew, disc, val)] for _ in range(nsets)]
+    outs = [[hip.DeviceBuffer(n) for n in (T * B * 4, T * B * 4, T * B * A * 4, (T + 1) * B * 4, 24)]
+            for _ in range(nsets)]
     H = _abi.VtraceHparams(rho_bar=1.0, c_bar=1.0, pg_rho_bar=1.0, lambda_=1.0,
                            baseline_cost=0.5, entropy_cost=0.01)
     ref = None
     for path in libs:
+      for variant in (args.variant or [0]):
         L = _abi.lib() if path is None else C.CDLL(os.path.abspath(path))
         if path is not None:
             for name, (argt, res) in _abi.SIGNATURES.items():
@@ -48,29 +54,32 @@ def main():
                     f = getattr(L, name)
                     f.restype, f.argtypes = res, argt
         wsb = L.fi_vtrace_workspace_bytes(T, B, A)
-        ws = hip.DeviceBuffer(wsb)
-        ws.zero()
+        wss = [hip.DeviceBuffer(wsb) for _ in range(nsets)]
+        for w in wss:
+            w.zero()
 
-        def launch():
-            rc = L.fi_vtrace_loss_fp32_variant(0, T, B, A, *[b.ptr for b in bufs], C.byref(H),
-                                               *[o.ptr for o in outs], ws.ptr, wsb, None)
+        def launch(i):
+            k = i % nsets
+            rc = L.fi_vtrace_loss_fp32_variant(variant, T, B, A, *[b.ptr for b in bufs[k]], C.byref(H),
+                                               *[o.ptr for o in outs[k]], wss[k].ptr, wsb, None)
             assert rc == 0, rc
 
-        for _ in range(5):
-            launch()
+        for i in range(max(5, nsets)):
+            launch(i)
         e0, e1 = hip.Event(), hip.Event()
         e0.record()
-        for _ in range(args.iters):
-            launch()
+        for i in range(args.iters):
+            launch(i)
         e1.record()
         hip.synchronize()
         ms = e0.elapsed_ms(e1) / args.iters
         gbs = (12 * A + 28) * T * B / (ms * 1e-3) / 1e9
-        dl = outs[2].download(np.float32, (T, B, A))
+        dl = outs[0][2].download(np.float32, (T, B, A))
         diff = 0.0 if ref is None else float(np.abs(dl - ref).max())
         ref = dl if ref is None else ref
-        print(f"{path or 'default'}: {ms * 1e3:.2f} us/launch  {gbs:.0f} GB/s  "
+        print(f"{path or 'default'} variant {variant} sets {nsets}: {ms * 1e3:.2f} us/launch  {gbs:.0f} GB/s  "
               f"({gbs / 8000:.1%} of 8 TB/s)  max|d dlogits| vs first {diff:.2e}", flush=True)
+        ws = wss[0]
         if args.stamps and wsb >= 8 * (1024 + (B // 8) * 20):
             nblk = B // 8
             st = ws.download(np.uint64, (wsb // 8,))[1024:1024 + nblk * 20].reshape(nblk, 20)

@@ -49,11 +49,14 @@ def _grad_close(a, b, what):
     assert d <= 1e-5 * np.linalg.norm(b) + 1e-7 * np.sqrt(b.size), f"{what}: |d| {d:.3e}, |ref| {np.linalg.norm(b):.3e}"
 
 
-@pytest.mark.parametrize("B,T,loss", [(64, 100, "mse"), (13, 1, "huber"), (40, 33, "mae")])
+@pytest.mark.parametrize("B,T,loss", [(64, 100, "mse"), (13, 1, "huber"), (40, 33, "mae"),
+                                      (301, 7, "mse"), (601, 5, "huber"), (1030, 3, "mse")])
 def test_farmer_step_vs_oracle_long_and_ragged(B, T, loss):
-    """T = 100 (SURVEY.md section 6's CPU measurement shape), T = 1, B not a multiple of the
-    recurrence kernel's 8 rows: every gradient tensor within 1e-5 relative L2 of the oracle
-    (absolute floor 1e-7 sqrt(n) for cancelling sums)."""
+    """T = 100 (SURVEY.md section 6's CPU measurement shape), T = 1, and the three shapes of the
+    register-resident recurrence kernels -- R = 1 row per workgroup (B <= 256), R = 2 (B <= 512:
+    301 leaves a half-empty last workgroup), R = 4 (601, 1030: ragged last workgroups, 1030 more
+    workgroups than CUs): every gradient tensor within 1e-5 relative L2 of the oracle (absolute
+    floor 1e-7 sqrt(n) for cancelling sums)."""
     from oracle import farmer_oracle as fo
     p0 = fo.gen_params(5)
     z, x, y = fo.gen_inputs(6, B, T)
