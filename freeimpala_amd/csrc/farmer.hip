@@ -71,15 +71,21 @@ __global__ void lstm_prep_kernel(const float* __restrict__ bih, const float* __r
 // rows' h (or dgates) sit in LDS as [k][R] and are read by wave-uniform broadcast
 // ds_read_b128; R rows are processed with packed fp32 FMAs. Two barriers per step.
 // Packed fp32 FMA with one weight broadcast to both halves: w holds two consecutive weights
-// (w[k], w[k+1]) as one VGPR pair; SEL picks which one multiplies both halves of h
-// (op_sel / op_sel_hi on src0), so the weights stay 128 registers and no pair is duplicated.
+// (w[k], w[k+1]) as one VGPR pair; SEL picks which one multiplies both halves of h. Written
+// as a shuffle the compiler folds into v_pk_fma_f32's op_sel / op_sel_hi on src0 (checked in
+// the .s: no duplicated pair), with the compiler's own hazard handling (an inline-asm form of
+// this instruction gave history-dependent wrong results on the GPU). lstm_opaque() below keeps
+// the broadcast from being hoisted out of the time loop as a loop-invariant pair per weight,
+// which doubles the weights' registers and spills.
 template <int SEL>
 __device__ __forceinline__ f32x2 pk_fma_bw(f32x2 w, f32x2 h, f32x2 acc) {
-    if constexpr (SEL == 0)
-        asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[0,1,1]" : "+v"(acc) : "v"(w), "v"(h));
-    else
-        asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,0,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "v"(w), "v"(h));
-    return acc;
+    return __builtin_elementwise_fma(__builtin_shufflevector(w, w, SEL, SEL), h, acc);
+}
+// per time step: the weights become opaque values (no instruction), so nothing derived from
+// them can be hoisted out of the t loop
+__device__ __forceinline__ void lstm_opaque(f32x2 (&w)[H / 2]) {
+#pragma unroll
+    for (int i = 0; i < H / 2; ++i) asm volatile("" : "+v"(w[i]));
 }
 __device__ __forceinline__ f32x2 pk_fma2(f32x2 w, f32x2 h, f32x2 acc) {
     return __builtin_elementwise_fma(w, h, acc);
@@ -166,6 +172,7 @@ __global__ __launch_bounds__(512) void lstm_fwd_reg_kernel(const float* __restri
     if (n < R * H) hs[iu * R + ir] = 0.f;
     __syncthreads();
     for (int t = 0; t < T; ++t) {
+        lstm_opaque(w);
         float acc[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) acc[r] = b0 + r < B ? xp[((size_t)(b0 + r) * T + t) * G + n] : 0.f;
@@ -220,6 +227,7 @@ __global__ __launch_bounds__(512) void lstm_bwd_reg_kernel(const float* __restri
     const bool ivalid = item && irow < B;
     float dh = ivalid ? dcat[(size_t)irow * CAT + u] : 0.f, dc = 0.f;
     for (int t = T - 1; t >= 0; --t) {
+        lstm_opaque(w);
         if (item) {
             if (t < T - 1) dh = (ps[(0 * R + ir) * H + u] + ps[(1 * R + ir) * H + u]) +
                                 (ps[(2 * R + ir) * H + u] + ps[(3 * R + ir) * H + u]);
@@ -563,11 +571,18 @@ extern "C" int fi_farmer_create(const fi_farmer_config* cfg, fi_farmer** out) {
         rc = fail(FI_ERR_HIP, "farmer_create: hipStreamCreate failed");
     if (rc == FI_OK && (hipEventCreate(&f->e0) != hipSuccess || hipEventCreate(&f->e1) != hipSuccess))
         rc = fail(FI_ERR_HIP, "farmer_create: hipEventCreate failed");
-    if (rc == FI_OK && (hipMemset(f->m, 0, P * 4) != hipSuccess || hipMemset(f->v, 0, P * 4) != hipSuccess ||
-                        hipMemset(f->params, 0, P * 4) != hipSuccess || hipMemset(f->grads, 0, P * 4) != hipSuccess ||
-                        hipMemset(f->z, 0, BT * IN * 4) != hipSuccess || hipMemset(f->x, 0, B * XD * 4) != hipSuccess ||
-                        hipMemset(f->y, 0, B * 4) != hipSuccess))
-        rc = fail(FI_ERR_HIP, "farmer_create: hipMemset failed");
+    // zero the state ON the handle's own stream and wait: the stream is non-blocking, so
+    // memsets on the legacy null stream would not be ordered before the set_params copy and
+    // the first step's kernels that follow on this stream (a late memset of the parameters
+    // then zeroes them under the step: history-dependent wrong results)
+    if (rc == FI_OK) {
+        hipStream_t s = f->stream;
+        if (hipMemsetAsync(f->m, 0, P * 4, s) != hipSuccess || hipMemsetAsync(f->v, 0, P * 4, s) != hipSuccess ||
+            hipMemsetAsync(f->params, 0, P * 4, s) != hipSuccess || hipMemsetAsync(f->grads, 0, P * 4, s) != hipSuccess ||
+            hipMemsetAsync(f->z, 0, BT * IN * 4, s) != hipSuccess || hipMemsetAsync(f->x, 0, B * XD * 4, s) != hipSuccess ||
+            hipMemsetAsync(f->y, 0, B * 4, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+            rc = fail(FI_ERR_HIP, "farmer_create: hipMemsetAsync failed");
+    }
     if (rc != FI_OK) {
         fi_farmer_destroy(f);
         return rc;
@@ -670,7 +685,10 @@ extern "C" int fi_farmer_tensor(fi_farmer* f, const char* name, void** ptr, size
     } t[] = {{"params", f->params, f->off.total * 4}, {"grads", f->grads, f->off.total * 4},
              {"values", f->val, B * 4},               {"z", f->z, BT * IN * 4},
              {"x", f->x, B * XD * 4},                 {"targets", f->y, B * 4},
-             {"gates", f->gates, BT * G * 4},         {"h_last", f->cat, B * CAT * 4}};
+             {"gates", f->gates, BT * G * 4},         {"h_last", f->cat, B * CAT * 4},
+             {"act1", f->act[1], B * DW * 4},         {"act2", f->act[2], B * DW * 4},
+             {"act3", f->act[3], B * DW * 4},         {"act4", f->act[4], B * DW * 4},
+             {"act5", f->act[5], B * DW * 4}};
     for (const E& e : t)
         if (std::strcmp(e.n, name) == 0) {
             *ptr = e.p;

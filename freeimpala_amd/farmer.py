@@ -157,6 +157,14 @@ class FarmerLstmModel:
         _abi.check(lib().fi_farmer_tensor(self._h, name.encode(), C.byref(p), C.byref(n)), "fi_farmer_tensor")
         return p.value, n.value
 
+    def tensor_array(self, name: str, shape, dtype=np.float32) -> np.ndarray:
+        """A copy of a named device tensor (fi_farmer_tensor) as a host array, after the
+        handle's stream has finished."""
+        p, n = self.tensor(name)
+        hip.synchronize()
+        a = hip.download_ptr(p, dtype, (n // np.dtype(dtype).itemsize,))
+        return a.reshape(shape)
+
     def _check_shapes(self, z, x, t=None):
         assert z.shape == (self.B, self.T, I_IN) and x.shape == (self.B, X_IN), (z.shape, x.shape)
         if t is not None:

@@ -70,7 +70,8 @@ int fi_farmer_train_step(fi_farmer* f, const float* z, const float* x, const flo
 int fi_farmer_forward(fi_farmer* f, const float* z, const float* x, int inputs_on_device,
                       float* values);
 /* introspection: device pointer / bytes of "params", "grads", "values", "z", "x",
- * "targets" (the handle's resident input buffers), "gates", "h_last" */
+ * "targets" (the handle's resident input buffers), "gates", "h_last", "act1".."act5" (the
+ * dense layers' ReLU outputs [B][512]) */
 int fi_farmer_tensor(fi_farmer* f, const char* name, void** dev_ptr, size_t* bytes);
 void* fi_farmer_stream(fi_farmer* f);
 /* Profiling (bench / roofline): with profiling on, every later train step records HIP events

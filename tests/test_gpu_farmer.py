@@ -68,12 +68,49 @@ def test_farmer_step_vs_oracle_long_and_ragged(B, T, loss):
     np.testing.assert_allclose(val, v_ref, rtol=1e-5, atol=1e-6)
     assert abs(lv - l_ref) <= 1e-5 * max(1.0, abs(l_ref))
     g = M.get_grads()
+    # the backward fed with the GPU's own dense activations: identical ReLU masks (at B in the
+    # hundreds an fp32 pre-activation within ~1e-7 of 0 lands on the other side of the mask than
+    # fp64's and moves one row of a weight gradient); the activations themselves are checked
+    acts_gpu = [M.tensor_array(f"act{l}", (B, 512)) for l in range(1, 6)]
+    for l in range(1, 6):
+        e = np.abs(acts_gpu[l - 1] - saved["acts"][l]).max() / max(1.0, np.abs(saved["acts"][l]).max())
+        assert e <= 1e-5, (l, e)
+    saved_gpu = dict(saved, acts=[saved["acts"][0]] + [a.astype(np.float64) for a in acts_gpu])
+    g_ref = fo.backward(p0, saved_gpu, dval)
     for n, (a, b, s) in fo.offsets().items():
         _grad_close(g[a:b], g_ref[a:b], n)
     # SGD: p1 = p0 - lr g exactly as torch's p.add_(g, alpha=-lr)
     p1 = M.get_params()
     np.testing.assert_allclose(p1, p0 + np.float32(-1e-2) * g, rtol=0, atol=1e-7)
     M.close()
+
+
+@pytest.mark.parametrize("B,T", [(301, 9), (601, 6)])
+def test_farmer_register_recurrence_is_deterministic(B, T):
+    """The R = 2 / R = 4 register-resident recurrences, run on handles created after the device
+    memory was filled with NaN garbage: every handle gives bit-identical values and gradients
+    (no read of uninitialised memory, no race between the item and matvec phases)."""
+    from freeimpala_amd import hip
+    from oracle import farmer_oracle as fo
+    junk = [hip.DeviceBuffer(64 << 20) for _ in range(4)]
+    for j in junk:
+        j.upload(np.full((64 << 20) // 4, np.nan, np.float32))
+    for j in junk:
+        j.free()
+    p0 = fo.gen_params(9)
+    z, x, y = fo.gen_inputs(10, B, T)
+    res = []
+    for _ in range(3):
+        M = _model(B, T, "mse", "sgd", 1e-2, p0)
+        lv, val = M.train_step(z, x, y, with_values=True)
+        res.append((lv, val.copy(), M.get_grads()))
+        M.close()
+    v_ref, _ = fo.forward(p0, z, x)
+    np.testing.assert_allclose(res[0][1], v_ref, rtol=1e-5, atol=1e-6)
+    for lv, val, g in res[1:]:
+        assert lv == res[0][0]
+        np.testing.assert_array_equal(val, res[0][1])
+        np.testing.assert_array_equal(g, res[0][2])
 
 
 def test_farmer_forward_equals_train_values_and_is_deterministic():
