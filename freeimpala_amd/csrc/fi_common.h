@@ -127,6 +127,20 @@ __device__ __forceinline__ void blds16(fi_i32x4 rsrc, uint32_t voff, uint32_t ld
         : "memory");
 }
 
+// the same with 4 bytes per lane: LDS (lds_base + 4 * lane)
+__device__ __forceinline__ void blds4(fi_i32x4 rsrc, uint32_t voff, uint32_t lds_base) {
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %3\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dword %1, %2, 0 offen lds\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(rsrc), "s"(lds_base)
+        : "memory");
+}
+
 template <typename T>
 __device__ __forceinline__ uint32_t lds_addr(T* p) {
     return (uint32_t)(uintptr_t)p;

@@ -507,33 +507,40 @@ __global__ __launch_bounds__(64 * VtLayout<A>::NW, VtLayout<A>::WPS) void vtrace
 }
 
 // ------------------------------------------------------------------------------------
-// Kernel 3 (vtrace_seq_kernel<A>, the default for T <= 128): one 256-thread workgroup owns
-// NB = 2 batch columns for the WHOLE sequence, so there is no chain of chunks inside a
-// workgroup -- the only serial dependency of V-trace (the scalar carry acc_{t+1}) is resolved
-// by one in-register scan plus one cross-wave combine. The two columns' pi and mu logits
-// (T rows x 144 B each, 28.8 KB at T = 100) arrive by LDS-DMA in one burst (1-KiB contiguous
-// LDS per wave instruction, 144-B contiguous global runs), the scalars straight into
-// registers; 32 KB of LDS per workgroup lets five workgroups share a CU (20 waves), so one
-// workgroup's burst overlaps four others' arithmetic and 2048 workgroups keep the DMA
-// engines busy through the whole launch.
+// Kernel 3 (vtrace_seq_kernel<A>, the default for T <= 128): a persistent 256-thread
+// workgroup walks column PAIRS p = lg, lg + G, ... and owns each pair for the WHOLE sequence,
+// so the only serial dependency of V-trace (the scalar carry acc_{t+1}) is resolved by one
+// in-register scan plus one cross-wave combine per pair -- no chain of time chunks.
+// A pair's data (pi and mu tiles: T rows x 144 B; the act / rew / disc / val columns:
+// T (+1) rows x 8 B) arrives by LDS-DMA into one of two slots (32 KB each at T = 100); the
+// next pair's DMA is issued right after the landing barrier, so it streams in while this
+// pair is computed. Two workgroups per CU (8 waves, 4 pair-slots of LDS). Pairs adjacent in
+// memory go to workgroups on the same XCD (xcd_remap), whose 144-B row runs share L2 lines.
 // Lane map: lane = j + 32 c, column c = lane >> 5, j = 0..31 the wave's rows in REVERSE time
 // (t = 32 w + 31 - j), so the reverse recurrence acc_t = d_t + g_t acc_{t+1} is a prefix
 // scan in lane order inside each 32-lane half: DPP row_shr:1/2/4/8 inside 16-lane rows, then
 // row_bcast:15 into the upper row (the classic gfx9 scan, affine operator), identity (0, 1)
 // shifted in at the edges. Wave totals cross waves through LDS (one barrier).
-// dlogits are written over the lane's own pi row in LDS and leave as 16-byte stores in the
-// global layout's 144-B runs. Algorithmic HBM traffic: 12A+28 bytes per (t,b), as kernel 1.
+// dlogits are written over the lane's own pi row in the slot and leave as 16-byte stores in
+// the global layout's 144-B runs. Loss partials stay in registers across pairs and are
+// reduced once per workgroup. vmcnt is counted per wave: every store instruction always
+// issues (lanes with t >= T write the scratch sink), so the wait for pair k+1's DMA leaves
+// exactly pair k's stores outstanding. Algorithmic HBM traffic: 12A+28 bytes per (t,b).
 // ------------------------------------------------------------------------------------
 template <int A>
 struct VtSeq {
-    static constexpr int NB = 2;                // batch columns per workgroup
+    static constexpr int NB = 2;                // batch columns per pair
     static constexpr int NT = 256;              // threads: 4 waves x 32 rows x 2 columns
     static constexpr int TMAX = NT / NB;        // 128 timesteps
     static constexpr int ROWB = NB * A * 4;     // bytes per t-row of a logits tile (144 at A=18)
     static constexpr int PPR = ROWB / 16;       // 16-B pieces per t-row
     static_assert(A % 2 == 0 && ROWB % 16 == 0, "pieces");
-    // LDS: pi tile [T][ROWB] | mu tile [T][ROWB] | wave totals [4 waves][2 (d, g)][NB] | loss scratch
-    static size_t lds_bytes(int T) { return (size_t)2 * T * ROWB + 4 * 2 * NB * 4 + 4 * 3 * 8; }
+    // slot: pi [T][ROWB] | mu [T][ROWB] | act [T][NB] | rew [T][NB] | disc [T][NB] | val [T+1][NB]
+    __host__ __device__ static int tile_bytes(int T) { return T * ROWB; }
+    __host__ __device__ static int col_bytes(int T) { return T * NB * 4; }
+    __host__ __device__ static int slot_bytes(int T) { return (2 * tile_bytes(T) + 4 * col_bytes(T) + NB * 4 + 15) & ~15; }
+    // two slots | wave totals [4][2][NB] | loss scratch [4][3] doubles
+    static size_t lds_bytes(int T) { return (size_t)2 * slot_bytes(T) + 4 * 2 * NB * 4 + 4 * 3 * 8; }
 };
 
 // identity-filled DPP move of a float (lanes whose source is out of range get `idf`)
@@ -550,150 +557,236 @@ __device__ __forceinline__ void vt_affine_step(float& D, float& G) {
     G = G * pg;
 }
 
+// DMA instructions of one pair, in one list: pi pieces (16 B x 64 lanes = 1 KiB each), mu
+// pieces, then the four scalar columns (4 B x 64 lanes = 256 B each); wave w issues the
+// entries i = w, w + 4, ... Returns how many it issued (wave-uniform).
 template <int A>
-__global__ __launch_bounds__(256, 5) void vtrace_seq_kernel(VtArgs a) {
+__device__ __forceinline__ int vt_seq_issue(const VtArgs& a, const fi_i32x4 (&rs)[6], uint32_t slot_lds, int T,
+                                            int b0, int w, int lane) {
+    using L = VtSeq<A>;
+    const int B = a.B;
+    const int np = T * L::PPR, nl = (np + 63) / 64;       // pieces / instructions per logits tile
+    const int nc = 2 * T, ncl = (nc + 63) / 64;           // words / instructions per scalar column
+    const int nv = 2 * (T + 1), nvl = (nv + 63) / 64;     // val has the bootstrap row
+    const int total = 2 * nl + 3 * ncl + nvl;
+    int n = 0;
+    for (int i = w; i < total; i += 4, ++n) {
+        if (i < 2 * nl) {
+            const int tile = i >= nl, ii = tile ? i - nl : i;
+            const int q = 64 * ii + lane;
+            const int qq = q < np ? q : np - 1;  // masked lanes re-read the last piece into the slack
+            const int row = qq / L::PPR, pc = qq - row * L::PPR;
+            const uint32_t off = (uint32_t)((row * B + b0) * A * 4 + pc * 16);
+            if (q < np) {  // wave-uniform branches: the descriptor must stay in SGPRs
+                const uint32_t dst = __builtin_amdgcn_readfirstlane(slot_lds + tile * L::tile_bytes(T) + 1024 * ii);
+                if (tile == 0) blds16(rs[0], off, dst);
+                else blds16(rs[1], off, dst);
+            }
+        } else {
+            const int k = i - 2 * nl;
+            const int col = k < 3 * ncl ? k / ncl : 3, ii = col < 3 ? k - col * ncl : k - 3 * ncl;
+            const int lim = col < 3 ? nc : nv;
+            const int q = 64 * ii + lane;
+            const int row = q >> 1;
+            const uint32_t off = (uint32_t)((row * B + b0 + (q & 1)) * 4);
+            const uint32_t dst =
+                __builtin_amdgcn_readfirstlane(slot_lds + 2 * L::tile_bytes(T) + col * L::col_bytes(T) + 256 * ii);
+            if (q < lim) {
+                if (col == 0) blds4(rs[2], off, dst);
+                else if (col == 1) blds4(rs[3], off, dst);
+                else if (col == 2) blds4(rs[4], off, dst);
+                else blds4(rs[5], off, dst);
+            }
+        }
+    }
+    return n;
+}
+
+template <int A>
+__global__ __launch_bounds__(256, 2) void vtrace_seq_kernel(VtArgs a) {
     using L = VtSeq<A>;
     extern __shared__ __attribute__((aligned(16))) char vsm[];
     const int T = a.T, B = a.B;
     const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
-    const int cb = xcd_remap(blockIdx.x, gridDim.x);
-    const int b0 = cb * L::NB;
+    const int G = gridDim.x, lg = xcd_remap(blockIdx.x, G);
+    const int npairs = B / L::NB;
     const int j = lane & 31, c = lane >> 5;
     const int t = 32 * w + 31 - j;
     const bool valid = t < T;
-    const int b = b0 + c;
     const int tt = valid ? t : T - 1;  // rows past T read a valid row, contribute identity
-    char* const pit = vsm;
-    char* const mut = vsm + (size_t)T * L::ROWB;
-    float* const tot = (float*)(vsm + (size_t)2 * T * L::ROWB);
-
-    // 1. the pi and mu tiles by LDS-DMA: piece q of a tile = row q / PPR, 16 B at (q % PPR) * 16
+    const int SB = L::slot_bytes(T);
+    float* const tot = (float*)(vsm + 2 * SB);
+    const uint32_t lds0 = lds_addr(vsm);
+    fi_i32x4 rs[6];
     {
-        const uint32_t lbytes = (uint32_t)T * B * A * 4;
-        const fi_i32x4 rpi = make_rsrc(a.pi, lbytes), rmu = make_rsrc(a.mu, lbytes);
-        const int npieces = T * L::PPR;
-        const uint32_t lds_pi = lds_addr(pit), lds_mu = lds_addr(mut);
-        for (int i = w; 64 * i < npieces; i += 4) {
-            const int q = 64 * i + lane;
-            if (q < npieces) {
-                const int row = q / L::PPR, pc = q - row * L::PPR;
-                const uint32_t off = (uint32_t)((row * B + b0) * A * 4 + pc * 16);
-                blds16(rpi, off, lds_pi + 1024 * i);
-                blds16(rmu, off, lds_mu + 1024 * i);
-            }
-        }
-    }
-    // 2. the scalars straight into registers (overlapping the DMA)
-    const size_t e = (size_t)tt * B + b;
-    int at = a.act[e];
-    const float rw = a.rew[e], g = a.disc[e], v = a.val[e], vn = a.val[e + B];
-    if (tid < L::NB) a.dval[(size_t)T * B + b0 + tid] = 0.f;
-    if (valid && (unsigned)at >= (unsigned)A) atomicAdd(a.bad, 1);
-    at = at < 0 ? 0 : (at >= A ? A - 1 : at);
-    wait_vmcnt(0);
-    lds_barrier();
-
-    // 3. softmax statistics of the lane's own row (as kernel 1)
-    constexpr float L2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
-    float* const zpi = (float*)(pit + (size_t)tt * L::ROWB) + c * A;
-    const float* const zmu = (const float*)(mut + (size_t)tt * L::ROWB) + c * A;
-    f32x2 zp2[A / 2], zm2[A / 2];
-#pragma unroll
-    for (int i = 0; i < A / 2; ++i) {
-        zp2[i] = *(const f32x2*)(zpi + 2 * i);
-        zm2[i] = *(const f32x2*)(zmu + 2 * i);
-    }
-    const float zpa = zpi[at], zma = zmu[at];
-    float mx = vt_max3(zp2[0].x, zp2[0].y, zp2[0].y), mm = vt_max3(zm2[0].x, zm2[0].y, zm2[0].y);
-#pragma unroll
-    for (int i = 1; i < A / 2; ++i) {
-        mx = vt_max3(mx, zp2[i].x, zp2[i].y);
-        mm = vt_max3(mm, zm2[i].x, zm2[i].y);
-    }
-    const f32x2 nmx = {-mx * L2E, -mx * L2E}, nmm = {-mm * L2E, -mm * L2E};
-    f32x2 e2[A / 2];
-    f32x2 sp2 = {0.f, 0.f}, sm2 = {0.f, 0.f}, sz2 = {0.f, 0.f};
-#pragma unroll
-    for (int i = 0; i < A / 2; ++i) {
-        const f32x2 ap = zp2[i] * L2E + nmx;
-        const f32x2 am = zm2[i] * L2E + nmm;
-        e2[i] = f32x2{VT_EXP2(ap.x), VT_EXP2(ap.y)};
-        sp2 += e2[i];
-        sz2 += e2[i] * zp2[i];
-        sm2 += f32x2{VT_EXP2(am.x), VT_EXP2(am.y)};
+        const uint32_t lbytes = (uint32_t)T * B * A * 4, sbytes = (uint32_t)T * B * 4;
+        rs[0] = make_rsrc(a.pi, lbytes);
+        rs[1] = make_rsrc(a.mu, lbytes);
+        rs[2] = make_rsrc(a.act, sbytes);
+        rs[3] = make_rsrc(a.rew, sbytes);
+        rs[4] = make_rsrc(a.disc, sbytes);
+        rs[5] = make_rsrc(a.val, sbytes + (uint32_t)B * 4);
     }
     const fi_vtrace_hparams hp = a.hp;
-    const float sp = sp2.x + sp2.y, sm = sm2.x + sm2.y;
-    const float lse = mx + VT_LOG2(sp) * LN2, lsem = mm + VT_LOG2(sm) * LN2;
-    const float inv = __builtin_amdgcn_rcpf(sp);
-    const float plogp = (sz2.x + sz2.y) * inv - lse;
-    const float lpa = zpa - lse, lma = zma - lsem;
-    const float ratio = VT_EXP(lpa - lma);
-    const float rho = fminf(hp.rho_bar, ratio);
-    const float cc = hp.lambda_ * fminf(hp.c_bar, ratio);
-    const float pgr = fminf(hp.pg_rho_bar, ratio);
-    const float d_own = valid ? rho * (rw + g * vn - v) : 0.f;
-    const float g_own = valid ? g * cc : 1.f;
+    // per-wave store instructions of one pair: vs, adv, dval + this wave's dlogits pieces
+    const int np = T * L::PPR;
+    int n_dl = 0;
+    for (int i = w; 64 * i < np; i += 4) ++n_dl;
+#ifdef FI_VTS_NOSTORE  // timing experiment: no output stores
+    const int n_st = 0;
+#else
+    const int n_st = 3 + n_dl;
+#endif
+    float pg = 0.f, base = 0.f, ent = 0.f;
+    float* const sink = a.sink + tid;  // stores of lanes with t >= T
 
-    // 4. prefix composition in lane order (= reverse time) inside each 32-lane column half
-    float D = d_own, G = g_own;
-    vt_affine_step<0x111>(D, G);          // row_shr:1
-    vt_affine_step<0x112>(D, G);          // row_shr:2
-    vt_affine_step<0x114>(D, G);          // row_shr:4
-    vt_affine_step<0x118>(D, G);          // row_shr:8
-    vt_affine_step<0x142, 0xa>(D, G);     // row_bcast:15 into rows 1 and 3 (lanes 16-31, 48-63)
-    // exclusive composition (the rows after t inside the wave): one lane up, identity at j = 0
-    float Dx = vt_dppf<0x138>(D, 0.f), Gx = vt_dppf<0x138>(G, 1.f);  // wave_shr:1
-    if (j == 0) {
-        Dx = 0.f;
-        Gx = 1.f;
-    }
-    if (j == 31) {  // the wave's total for column c
-        tot[(w * 2 + 0) * L::NB + c] = D;
-        tot[(w * 2 + 1) * L::NB + c] = G;
-    }
-    __syncthreads();
-    float x = 0.f;  // acc at t = 32 (w + 1): later waves composed onto the bootstrap acc_T = 0
-#pragma unroll
-    for (int w2 = 3; w2 >= 0; --w2)
-        if (w2 > w) x = tot[(w2 * 2 + 0) * L::NB + c] + tot[(w2 * 2 + 1) * L::NB + c] * x;
-    const float acc_nx = Dx + Gx * x;  // acc_{t+1}
-    const float acc = d_own + g_own * acc_nx;
-    const float vs_t = v + acc;
-    const float adv = pgr * (rw + g * (vn + acc_nx) - v);
-    const float dv = -hp.baseline_cost * acc;
+    int k = 0;
+    int p = lg;
+#ifndef FI_VTS_NODMA
+    if (p < npairs) vt_seq_issue<A>(a, rs, lds0, T, L::NB * p, w, lane);
+#endif
+    for (; p < npairs; p += G, ++k) {
+        const int b0 = L::NB * p, b = b0 + c;
+        char* const sl = vsm + (k & 1) * SB;
+        // this pair's DMA landed (the previous pair's stores may still be in flight)
+        wait_vmcnt(k > 0 ? n_st : 0);
+        lds_barrier();  // B1: slot k&1 landed for every wave; slot (k+1)&1's last reads done
+#ifndef FI_VTS_NODMA  // timing experiment: no input DMA (the slots hold whatever is there)
+        if (p + G < npairs) vt_seq_issue<A>(a, rs, lds0 + ((k + 1) & 1) * SB, T, L::NB * (p + G), w, lane);
+#endif
+        if (tid < L::NB) a.dval[(size_t)T * B + b0 + tid] = 0.f;  // the bootstrap row (not counted: see below)
 
-    // 5. dlogits over the lane's own pi row: dz_i = e_i (alpha + beta z_i) - adv [i = a_t]
-    {
-        const float ec = hp.entropy_cost;
-        const float al = inv * (adv - ec * (plogp + lse)), be = inv * ec;
-        const f32x2 al2 = {al, al};
-        if (valid) {
+        // scalars of the lane's (t, b)
+        const int* sact = (const int*)(sl + 2 * L::tile_bytes(T));
+        const float* srew = (const float*)(sl + 2 * L::tile_bytes(T) + L::col_bytes(T));
+        const float* sdisc = (const float*)(sl + 2 * L::tile_bytes(T) + 2 * L::col_bytes(T));
+        const float* sval = (const float*)(sl + 2 * L::tile_bytes(T) + 3 * L::col_bytes(T));
+#ifdef FI_VTS_NODMA
+        int at = sact[2 * tt + c] & 7;
+#else
+        int at = sact[2 * tt + c];
+#endif
+        const float rw = srew[2 * tt + c], g = sdisc[2 * tt + c], v = sval[2 * tt + c], vn = sval[2 * tt + 2 + c];
+        if (valid && (unsigned)at >= (unsigned)A) atomicAdd(a.bad, 1);
+        at = at < 0 ? 0 : (at >= A ? A - 1 : at);
+
+        // softmax statistics of the lane's own row (as kernel 1)
+        constexpr float L2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
+        float* const zpi = (float*)(sl + (size_t)tt * L::ROWB) + c * A;
+        const float* const zmu = (const float*)(sl + L::tile_bytes(T) + (size_t)tt * L::ROWB) + c * A;
+        f32x2 zp2[A / 2], zm2[A / 2];
 #pragma unroll
-            for (int i = 0; i < A / 2; ++i) *(f32x2*)(zpi + 2 * i) = e2[i] * (zp2[i] * be + al2);
-            zpi[at] -= adv;
+        for (int i = 0; i < A / 2; ++i) {
+#ifdef FI_VTS_NOCOMP  // timing experiment: no logits reads (softmax on constants)
+            zp2[i] = f32x2{0.f, (float)i};
+            zm2[i] = f32x2{(float)i, 0.f};
+#else
+            zp2[i] = *(const f32x2*)(zpi + 2 * i);
+            zm2[i] = *(const f32x2*)(zmu + 2 * i);
+#endif
         }
-    }
-    if (valid) {
-        VT_ST(vs_t, a.vs + e);
-        VT_ST(adv, a.adv + e);
-        VT_ST(dv, a.dval + e);
-    }
-    float pg = valid ? -adv * lpa : 0.f, base = valid ? 0.5f * acc * acc : 0.f, ent = valid ? plogp : 0.f;
-    lds_barrier();  // dlogits rows complete
+        const float zpa = zpi[at], zma = zmu[at];
+        float mx = vt_max3(zp2[0].x, zp2[0].y, zp2[0].y), mm = vt_max3(zm2[0].x, zm2[0].y, zm2[0].y);
+#pragma unroll
+        for (int i = 1; i < A / 2; ++i) {
+            mx = vt_max3(mx, zp2[i].x, zp2[i].y);
+            mm = vt_max3(mm, zm2[i].x, zm2[i].y);
+        }
+        const f32x2 nmx = {-mx * L2E, -mx * L2E}, nmm = {-mm * L2E, -mm * L2E};
+        f32x2 e2[A / 2];
+        f32x2 sp2 = {0.f, 0.f}, sm2 = {0.f, 0.f}, sz2 = {0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < A / 2; ++i) {
+            const f32x2 ap = zp2[i] * L2E + nmx;
+            const f32x2 am = zm2[i] * L2E + nmm;
+            e2[i] = f32x2{VT_EXP2(ap.x), VT_EXP2(ap.y)};
+            sp2 += e2[i];
+            sz2 += e2[i] * zp2[i];
+            sm2 += f32x2{VT_EXP2(am.x), VT_EXP2(am.y)};
+        }
+        const float sp = sp2.x + sp2.y, sm = sm2.x + sm2.y;
+        const float lse = mx + VT_LOG2(sp) * LN2, lsem = mm + VT_LOG2(sm) * LN2;
+        const float inv = __builtin_amdgcn_rcpf(sp);
+        const float plogp = (sz2.x + sz2.y) * inv - lse;
+        const float lpa = zpa - lse, lma = zma - lsem;
+        const float ratio = VT_EXP(lpa - lma);
+        const float rho = fminf(hp.rho_bar, ratio);
+        const float cc = hp.lambda_ * fminf(hp.c_bar, ratio);
+        const float pgr = fminf(hp.pg_rho_bar, ratio);
+        const float d_own = valid ? rho * (rw + g * vn - v) : 0.f;
+        const float g_own = valid ? g * cc : 1.f;
 
-    // 6. the dlogits tile out in the global layout (144-B runs), 16 B per lane
-    {
-        const int npieces = T * L::PPR;
-        for (int i = w; 64 * i < npieces; i += 4) {
+        // prefix composition in lane order (= reverse time) inside each 32-lane column half
+        float D = d_own, Gm = g_own;
+        vt_affine_step<0x111>(D, Gm);       // row_shr:1
+        vt_affine_step<0x112>(D, Gm);       // row_shr:2
+        vt_affine_step<0x114>(D, Gm);       // row_shr:4
+        vt_affine_step<0x118>(D, Gm);       // row_shr:8
+        vt_affine_step<0x142, 0xa>(D, Gm);  // row_bcast:15 into rows 1 and 3 (lanes 16-31, 48-63)
+        // exclusive composition (the rows after t inside the wave): one lane up, identity at j = 0
+        float Dx = vt_dppf<0x138>(D, 0.f), Gx = vt_dppf<0x138>(Gm, 1.f);  // wave_shr:1
+        if (j == 0) {
+            Dx = 0.f;
+            Gx = 1.f;
+        }
+        if (j == 31) {  // the wave's total for column c
+            tot[(w * 2 + 0) * L::NB + c] = D;
+            tot[(w * 2 + 1) * L::NB + c] = Gm;
+        }
+        lds_barrier();  // B2: wave totals visible
+        float x = 0.f;  // acc at t = 32 (w + 1): later waves composed onto the bootstrap acc_T = 0
+#pragma unroll
+        for (int w2 = 3; w2 >= 0; --w2)
+            if (w2 > w) x = tot[(w2 * 2 + 0) * L::NB + c] + tot[(w2 * 2 + 1) * L::NB + c] * x;
+        const float acc_nx = Dx + Gx * x;  // acc_{t+1}
+        const float acc = d_own + g_own * acc_nx;
+        const float vs_t = v + acc;
+        const float adv = pgr * (rw + g * (vn + acc_nx) - v);
+        const float dv = -hp.baseline_cost * acc;
+
+        // dlogits over the lane's own pi row: dz_i = e_i (alpha + beta z_i) - adv [i = a_t]
+        {
+            const float ec = hp.entropy_cost;
+            const float al = inv * (adv - ec * (plogp + lse)), be = inv * ec;
+            const f32x2 al2 = {al, al};
+            if (valid) {
+#pragma unroll
+                for (int i = 0; i < A / 2; ++i) *(f32x2*)(zpi + 2 * i) = e2[i] * (zp2[i] * be + al2);
+                zpi[at] -= adv;
+            }
+        }
+        if (valid) {
+            pg += -adv * lpa;
+            base += 0.5f * acc * acc;
+            ent += plogp;
+        }
+#ifndef FI_VTS_NOSTORE
+        {  // every lane stores (the sink takes rows t >= T), so each wave issues exactly 3 here
+            const size_t e = (size_t)tt * B + b;
+            VT_ST(vs_t, valid ? a.vs + e : sink);
+            VT_ST(adv, valid ? a.adv + e : sink);
+            VT_ST(dv, valid ? a.dval + e : sink);
+        }
+#else
+        asm volatile("" ::"v"(vs_t), "v"(adv), "v"(dv));
+#endif
+        lds_barrier();  // B3: the slot's dlogits rows complete
+
+        // the dlogits tile out in the global layout (144-B runs), 16 B per lane
+#ifndef FI_VTS_NOSTORE
+        for (int i = w; 64 * i < np; i += 4) {
             const int q = 64 * i + lane;
-            if (q < npieces) {
+            if (q < np) {
                 const int row = q / L::PPR, pc = q - row * L::PPR;
-                const f32x4 d4 = *(const f32x4*)(pit + 16 * q);
+                const f32x4 d4 = *(const f32x4*)(sl + 16 * q);
                 VT_ST(d4, (f32x4*)(a.dlog + (size_t)(row * B + b0) * A) + pc);
             }
         }
+#endif
+        // the bootstrap-row store above is the one VMEM op not in n_st: it was issued BEFORE
+        // this pair's stores, i.e. it is older than them and retired by the next wait as well
     }
+    __syncthreads();
     // per-workgroup loss partials (summed in a fixed order later, as kernel 1)
     block_reduce3((double)pg, (double)base, (double)ent, (double*)(tot + 4 * 2 * L::NB),
                   a.part + (size_t)blockIdx.x * 3);
@@ -718,7 +811,7 @@ __global__ __launch_bounds__(256) void vtrace_finalize_kernel(const double* __re
 // ------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------
-static size_t vt_nblk_max(int B) { return (size_t)std::max((B + 1) / 2, (B + 255) / 256); }
+static size_t vt_nblk_max(int B) { return (size_t)std::max({(B + 7) / 8, (B + 255) / 256, 2 * 1024}); }
 
 // workspace: [sink floats][loss partials, 256-B padded][int bad-action counter, 256 B]
 static size_t vt_part_bytes(int B) { return (vt_nblk_max(B) * 3 * sizeof(double) + 255) & ~(size_t)255; }
@@ -738,6 +831,17 @@ static void launch_lds(const VtArgs& a, int nblk, hipStream_t s) {
 template <int A>
 static void launch_seq(const VtArgs& a, int nblk, hipStream_t s) {
     hipLaunchKernelGGL(vtrace_seq_kernel<A>, dim3(nblk), dim3(VtSeq<A>::NT), VtSeq<A>::lds_bytes(a.T), s, a);
+}
+// persistent grid of the sequence kernel: two workgroups per CU (LDS: two pair slots each)
+static int seq_grid(int B) {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        hipDeviceProp_t prop;
+        cus = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+                  ? prop.multiProcessorCount : 256;
+    }
+    return std::max(1, std::min(B / 2, 2 * cus));
 }
 
 static bool lds_supported(int A, int B) { return B % 8 == 0 && A % 2 == 0 && A >= 2 && A <= 20; }
@@ -772,7 +876,7 @@ int vtrace_launch(int variant, int T, int B, int A, const float* pi, const float
     if (variant == 3 || (variant == 0 && seq_ok)) {
         FI_REQUIRE(vs && adv, "vtrace: sequence kernel writes vs and pg_adv (non-null)");
         FI_REQUIRE(((uintptr_t)pi | (uintptr_t)mu | (uintptr_t)dlog) % 16 == 0, "vtrace: needs 16-byte aligned logits");
-        const int nblk = B / 2;
+        const int nblk = seq_grid(B);
         switch (A) {
             case 2: launch_seq<2>(a, nblk, stream); break;
             case 4: launch_seq<4>(a, nblk, stream); break;

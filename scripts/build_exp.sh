@@ -1,14 +1,19 @@
 #!/bin/bash
-# build_exp.sh NAME [-DMACRO ...] -- experiment library build/ab/lib_NAME.so: atari_fr.hip
-# (or SRC=<file>) recompiled with the given macros, linked with the product objects of `make`
-# (A/B only; build/ab travels to the GPU box, build/exp does not).
+# build_exp.sh NAME [-DMACRO ...] -- experiment library build/ab/lib_NAME.so: one source
+# (SRC=<file>, default freeimpala_amd/csrc/atari_fr.hip) recompiled with the given macros and
+# linked with the product objects of `make` in place of that source's own object (A/B only;
+# build/ab travels to the GPU box, build/exp does not).
 set -e
 cd "$(dirname "$0")/.."
 n=$1; shift
 SRC=${SRC:-freeimpala_amd/csrc/atari_fr.hip}
+base=$(basename "$SRC")
 mkdir -p build/ab
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Iinclude -Ifreeimpala_amd/csrc \
-  -Wno-unused-result -Wno-unused-value -munsafe-fp-atomics "$@" -x hip -c "$SRC" -o build/ab/fr_$n.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o build/ab/lib_$n.so build/obj/farmer.hip.o build/obj/vtrace.hip.o \
-  build/obj/gemm_f32.hip.o build/obj/misc.hip.o build/obj/atari.hip.o build/ab/fr_$n.o build/obj/fc_gemm.hip.o \
-  build/obj/fc_blaslt.cpp.o build/obj/learner.cpp.o -L/opt/rocm/lib -lrccl -lhipblaslt -Wl,-rpath,/opt/rocm/lib
+  -Wno-unused-result -Wno-unused-value -munsafe-fp-atomics "$@" -x hip -c "$SRC" -o build/ab/x_$n.o
+objs=""
+for o in farmer.hip vtrace.hip gemm_f32.hip misc.hip atari.hip atari_fr.hip fc_gemm.hip fc_blaslt.cpp learner.cpp; do
+  if [ "$o" = "$base" ]; then objs="$objs build/ab/x_$n.o"; else objs="$objs build/obj/$o.o"; fi
+done
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o build/ab/lib_$n.so $objs \
+  -L/opt/rocm/lib -lrccl -lhipblaslt -Wl,-rpath,/opt/rocm/lib
