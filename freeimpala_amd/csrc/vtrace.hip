@@ -535,10 +535,13 @@ struct VtSeq {
     static constexpr int ROWB = NB * A * 4;     // bytes per t-row of a logits tile (144 at A=18)
     static constexpr int PPR = ROWB / 16;       // 16-B pieces per t-row
     static_assert(A % 2 == 0 && ROWB % 16 == 0, "pieces");
-    // slot: pi [T][ROWB] | mu [T][ROWB] | act [T][NB] | rew [T][NB] | disc [T][NB] | val [T+1][NB]
-    __host__ __device__ static int tile_bytes(int T) { return T * ROWB; }
-    __host__ __device__ static int col_bytes(int T) { return T * NB * 4; }
-    __host__ __device__ static int slot_bytes(int T) { return (2 * tile_bytes(T) + 4 * col_bytes(T) + NB * 4 + 15) & ~15; }
+    // slot: pi [T][ROWB] | mu [T][ROWB] | act [T][NB] | rew [T][NB] | disc [T][NB] | val [T+1][NB],
+    // each region padded to whole DMA instructions (1 KiB / 256 B), so the lanes of a tile's last
+    // instruction that run past its end read zeros (out-of-range offset) into the padding and
+    // every lane can issue
+    __host__ __device__ static int tile_bytes(int T) { return (T * ROWB + 1023) & ~1023; }
+    __host__ __device__ static int col_bytes(int T) { return (T * NB * 4 + NB * 4 + 255) & ~255; }
+    __host__ __device__ static int slot_bytes(int T) { return 2 * tile_bytes(T) + 4 * col_bytes(T); }
     // two slots | wave totals [4][2][NB] | loss scratch [4][3] doubles
     static size_t lds_bytes(int T) { return (size_t)2 * slot_bytes(T) + 4 * 2 * NB * 4 + 4 * 3 * 8; }
 };
@@ -557,49 +560,34 @@ __device__ __forceinline__ void vt_affine_step(float& D, float& G) {
     G = G * pg;
 }
 
-// DMA instructions of one pair, in one list: pi pieces (16 B x 64 lanes = 1 KiB each), mu
-// pieces, then the four scalar columns (4 B x 64 lanes = 256 B each); wave w issues the
-// entries i = w, w + 4, ... Returns how many it issued (wave-uniform).
+// DMA of one pair into a slot: the pi and mu tiles' 1-KiB pieces ii = w, w + 4, ... (16 B per
+// lane, the piece's 64 lanes cover 7 1/9 rows of 144 B), and scalar column w (act / rew / disc /
+// val for waves 0..3: 4 B per lane, 256 B per instruction). Lanes past a tile's end read zeros
+// (FI_OOB) into the slot's padding, so every instruction issues with all lanes. Offsets need a
+// constant division (by 9) only; the stores' vmcnt bookkeeping does not depend on this count.
 template <int A>
-__device__ __forceinline__ int vt_seq_issue(const VtArgs& a, const fi_i32x4 (&rs)[6], uint32_t slot_lds, int T,
-                                            int b0, int w, int lane) {
+__device__ __forceinline__ void vt_seq_issue(const fi_i32x4 (&rs)[6], uint32_t slot_lds, int T, int B, int w,
+                                             int lane, int b0) {
     using L = VtSeq<A>;
-    const int B = a.B;
-    const int np = T * L::PPR, nl = (np + 63) / 64;       // pieces / instructions per logits tile
-    const int nc = 2 * T, ncl = (nc + 63) / 64;           // words / instructions per scalar column
-    const int nv = 2 * (T + 1), nvl = (nv + 63) / 64;     // val has the bootstrap row
-    const int total = 2 * nl + 3 * ncl + nvl;
-    int n = 0;
-    for (int i = w; i < total; i += 4, ++n) {
-        if (i < 2 * nl) {
-            const int tile = i >= nl, ii = tile ? i - nl : i;
-            const int q = 64 * ii + lane;
-            const int qq = q < np ? q : np - 1;  // masked lanes re-read the last piece into the slack
-            const int row = qq / L::PPR, pc = qq - row * L::PPR;
-            const uint32_t off = (uint32_t)((row * B + b0) * A * 4 + pc * 16);
-            if (q < np) {  // wave-uniform branches: the descriptor must stay in SGPRs
-                const uint32_t dst = __builtin_amdgcn_readfirstlane(slot_lds + tile * L::tile_bytes(T) + 1024 * ii);
-                if (tile == 0) blds16(rs[0], off, dst);
-                else blds16(rs[1], off, dst);
-            }
-        } else {
-            const int k = i - 2 * nl;
-            const int col = k < 3 * ncl ? k / ncl : 3, ii = col < 3 ? k - col * ncl : k - 3 * ncl;
-            const int lim = col < 3 ? nc : nv;
-            const int q = 64 * ii + lane;
-            const int row = q >> 1;
-            const uint32_t off = (uint32_t)((row * B + b0 + (q & 1)) * 4);
-            const uint32_t dst =
-                __builtin_amdgcn_readfirstlane(slot_lds + 2 * L::tile_bytes(T) + col * L::col_bytes(T) + 256 * ii);
-            if (q < lim) {
-                if (col == 0) blds4(rs[2], off, dst);
-                else if (col == 1) blds4(rs[3], off, dst);
-                else if (col == 2) blds4(rs[4], off, dst);
-                else blds4(rs[5], off, dst);
-            }
-        }
+    const int np = T * L::PPR, nl = (np + 63) / 64;
+    const uint32_t dl = (uint32_t)b0 * A * 4;
+    for (int ii = w; ii < nl; ii += 4) {
+        const int q = 64 * ii + lane;
+        const int row = q / L::PPR, pc = q - row * L::PPR;
+        const uint32_t voff = q < np ? (uint32_t)(row * B * A * 4 + pc * 16) + dl : FI_OOB;
+        blds16(rs[0], voff, __builtin_amdgcn_readfirstlane(slot_lds + 1024 * ii));
+        blds16(rs[1], voff, __builtin_amdgcn_readfirstlane(slot_lds + L::tile_bytes(T) + 1024 * ii));
     }
-    return n;
+    const int lim = w < 3 ? 2 * T : 2 * (T + 1), ncl = (2 * (T + 1) + 63) / 64;
+    fi_i32x4 rc = w == 0 ? rs[2] : (w == 1 ? rs[3] : (w == 2 ? rs[4] : rs[5]));
+#pragma unroll
+    for (int e = 0; e < 4; ++e) rc[e] = __builtin_amdgcn_readfirstlane(rc[e]);
+    const uint32_t cbase = slot_lds + 2 * L::tile_bytes(T) + w * L::col_bytes(T);
+    for (int ii = 0; ii < ncl; ++ii) {
+        const int q = 64 * ii + lane;
+        const uint32_t voff = q < lim ? (uint32_t)(((q >> 1) * B + b0 + (q & 1)) * 4) : FI_OOB;
+        blds4(rc, voff, __builtin_amdgcn_readfirstlane(cbase + 256 * ii));
+    }
 }
 
 template <int A>
@@ -643,7 +631,7 @@ __global__ __launch_bounds__(256, 2) void vtrace_seq_kernel(VtArgs a) {
     int k = 0;
     int p = lg;
 #ifndef FI_VTS_NODMA
-    if (p < npairs) vt_seq_issue<A>(a, rs, lds0, T, L::NB * p, w, lane);
+    if (p < npairs) vt_seq_issue<A>(rs, lds0, T, B, w, lane, L::NB * p);
 #endif
     for (; p < npairs; p += G, ++k) {
         const int b0 = L::NB * p, b = b0 + c;
@@ -652,7 +640,7 @@ __global__ __launch_bounds__(256, 2) void vtrace_seq_kernel(VtArgs a) {
         wait_vmcnt(k > 0 ? n_st : 0);
         lds_barrier();  // B1: slot k&1 landed for every wave; slot (k+1)&1's last reads done
 #ifndef FI_VTS_NODMA  // timing experiment: no input DMA (the slots hold whatever is there)
-        if (p + G < npairs) vt_seq_issue<A>(a, rs, lds0 + ((k + 1) & 1) * SB, T, L::NB * (p + G), w, lane);
+        if (p + G < npairs) vt_seq_issue<A>(rs, lds0 + ((k + 1) & 1) * SB, T, B, w, lane, L::NB * (p + G));
 #endif
         if (tid < L::NB) a.dval[(size_t)T * B + b0 + tid] = 0.f;  // the bootstrap row (not counted: see below)
 
@@ -870,10 +858,11 @@ int vtrace_launch(int variant, int T, int B, int A, const float* pi, const float
     // the LDS kernel's buffer descriptors and DMA offsets are 32-bit: T*B*A*4 must stay
     // below 2^31 bytes (else the column kernel, 64-bit indexing, runs)
     const bool fits32 = (size_t)T * B * A * sizeof(float) < ((size_t)1 << 31);
-    // variant 3 (whole-sequence workgroups) is the default where it applies: T <= 128
+    // variant 3 (whole-sequence workgroups) on request only: measured slower than the chunked
+    // kernel 1 ("V-trace: the whole-sequence kernel")
     const bool seq_ok = lds_supported(A, B) && fits32 && T <= 128 && B % 2 == 0;
     FI_REQUIRE(!(variant == 3 && !seq_ok), "vtrace: sequence kernel needs T<=128, B%8==0, even A<=20");
-    if (variant == 3 || (variant == 0 && seq_ok)) {
+    if (variant == 3) {
         FI_REQUIRE(vs && adv, "vtrace: sequence kernel writes vs and pg_adv (non-null)");
         FI_REQUIRE(((uintptr_t)pi | (uintptr_t)mu | (uintptr_t)dlog) % 16 == 0, "vtrace: needs 16-byte aligned logits");
         const int nblk = seq_grid(B);
