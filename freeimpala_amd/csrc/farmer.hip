@@ -98,45 +98,67 @@ __device__ __forceinline__ f32x2 pk_fma2(f32x2 w, f32x2 h, f32x2 acc) {
 // (broadcast reads: every lane of a wave reads the same address)
 template <int R>
 __device__ __forceinline__ void lstm_matvec(const f32x2 (&w)[H / 2], const float* v, float (&acc)[R]) {
-    if constexpr (R == 1) {
-        f32x2 a0 = {acc[0], 0.f}, a1 = {0.f, 0.f};  // lanes: k even / k odd
+    // k in groups of GK; the LDS reads of group g + 1 are issued before group g's FMAs (a fence
+    // between them keeps the compiler from hoisting all reads of the unrolled loop), so each
+    // group's read latency hides behind the previous group's FMAs
+    constexpr int GK = R == 4 ? 4 : 8;       // k per group
+    constexpr int NR = GK * R / 4;           // ds_read_b128 per group
+    constexpr int NG = H / GK;
+    f32x4v buf[2][NR];
+    auto load = [&](int g, f32x4v* d) {
 #pragma unroll
-        for (int k = 0; k < H; k += 4) {
-            const f32x4v hv = *(const f32x4v*)&v[k];
-            a0 = pk_fma2(w[k / 2], f32x2{hv.x, hv.y}, a0);
-            a1 = pk_fma2(w[k / 2 + 1], f32x2{hv.z, hv.w}, a1);
-            if ((k & 31) == 28) FI_SCHED_FENCE();
+        for (int i = 0; i < NR; ++i) d[i] = *(const f32x4v*)&v[g * GK * R + 4 * i];
+    };
+    f32x2 a0, a1;
+    if constexpr (R == 1) {
+        a0 = f32x2{acc[0], 0.f};
+        a1 = f32x2{0.f, 0.f};
+    } else if constexpr (R == 2) {
+        a0 = f32x2{acc[0], acc[1]};
+        a1 = f32x2{0.f, 0.f};
+    } else {
+        a0 = f32x2{acc[0], acc[1]};
+        a1 = f32x2{acc[2], acc[3]};
+    }
+    load(0, buf[0]);
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+        if (g + 1 < NG) load(g + 1, buf[(g + 1) & 1]);
+        FI_SCHED_FENCE();
+        const f32x4v* cur = buf[g & 1];
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+            const f32x4v hv = cur[i];
+            if constexpr (R == 1) {  // v[k..k+3]: k = g GK + 4 i
+                const int k = g * GK + 4 * i;
+                a0 = pk_fma2(w[k / 2], f32x2{hv.x, hv.y}, a0);
+                a1 = pk_fma2(w[k / 2 + 1], f32x2{hv.z, hv.w}, a1);
+            } else if constexpr (R == 2) {  // v[k][0..1], v[k+1][0..1]: k = g GK + 2 i
+                const int k = g * GK + 2 * i;
+                a0 = pk_fma_bw<0>(w[k / 2], f32x2{hv.x, hv.y}, a0);
+                a1 = pk_fma_bw<1>(w[k / 2], f32x2{hv.z, hv.w}, a1);
+            } else if (i % 2 == 0) {  // v[k][0..3], v[k+1][0..3]: k = g GK + i (even)
+                const int k = g * GK + i;
+                const f32x4v h1 = cur[i + 1];
+                a0 = pk_fma_bw<0>(w[k / 2], f32x2{hv.x, hv.y}, a0);
+                a1 = pk_fma_bw<0>(w[k / 2], f32x2{hv.z, hv.w}, a1);
+                a0 = pk_fma_bw<1>(w[k / 2], f32x2{h1.x, h1.y}, a0);
+                a1 = pk_fma_bw<1>(w[k / 2], f32x2{h1.z, h1.w}, a1);
+            }
         }
+    }
+    if constexpr (R == 1) {
         const f32x2 a = a0 + a1;
         acc[0] = a.x + a.y;
     } else if constexpr (R == 2) {
-        f32x2 a0 = {acc[0], acc[1]}, a1 = {0.f, 0.f};  // rows 0, 1; chains over k even / odd
-#pragma unroll
-        for (int k = 0; k < H; k += 2) {
-            const f32x4v hv = *(const f32x4v*)&v[2 * k];  // v[k][0..1], v[k+1][0..1]
-            a0 = pk_fma_bw<0>(w[k / 2], f32x2{hv.x, hv.y}, a0);
-            a1 = pk_fma_bw<1>(w[k / 2], f32x2{hv.z, hv.w}, a1);
-            if ((k & 15) == 14) FI_SCHED_FENCE();
-        }
         const f32x2 a = a0 + a1;
         acc[0] = a.x;
         acc[1] = a.y;
     } else {
-        f32x2 a01 = {acc[0], acc[1]}, a23 = {acc[2], acc[3]};
-#pragma unroll
-        for (int k = 0; k < H; k += 2) {
-            const f32x4v h0 = *(const f32x4v*)&v[4 * k];  // v[k][0..3]
-            const f32x4v h1 = *(const f32x4v*)&v[4 * k + 4];
-            a01 = pk_fma_bw<0>(w[k / 2], f32x2{h0.x, h0.y}, a01);
-            a23 = pk_fma_bw<0>(w[k / 2], f32x2{h0.z, h0.w}, a23);
-            a01 = pk_fma_bw<1>(w[k / 2], f32x2{h1.x, h1.y}, a01);
-            a23 = pk_fma_bw<1>(w[k / 2], f32x2{h1.z, h1.w}, a23);
-            if ((k & 7) == 6) FI_SCHED_FENCE();
-        }
-        acc[0] = a01.x;
-        acc[1] = a01.y;
-        acc[2] = a23.x;
-        acc[3] = a23.y;
+        acc[0] = a0.x;
+        acc[1] = a0.y;
+        acc[2] = a1.x;
+        acc[3] = a1.y;
     }
 }
 
