@@ -1,7 +1,8 @@
 """Build identity of libfi_learner.so's sources, used to stamp counter passes.
 
-`source_hash()` is a sha256 over every file the library is built from (freeimpala_amd/csrc/*,
-include/fi_learner.h, include/fi_farmer.h, the Makefile), so a rocprofv3 PMC summary under
+`source_hash()` is a sha256 over every file the learner step's kernels are built from
+(freeimpala_amd/csrc/* except the FarmerLstm step's farmer.hip, include/fi_learner.h, the
+Makefile; the learner never launches a farmer kernel), so a rocprofv3 PMC summary under
 profiles/ can be matched to the exact kernels a bench line timed: bench.py attaches counter
 fields (HBM traffic, MFMA utilisation) only from a summary whose `_build.source_hash` equals the
 hash of the tree it runs from, and reports them as null otherwise.
@@ -17,7 +18,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def source_files():
     files = sorted(glob.glob(os.path.join(ROOT, "freeimpala_amd", "csrc", "*")))
-    files += [os.path.join(ROOT, p) for p in ("include/fi_learner.h", "include/fi_farmer.h", "Makefile")]
+    files = [f for f in files if os.path.basename(f) != "farmer.hip"]
+    files += [os.path.join(ROOT, p) for p in ("include/fi_learner.h", "Makefile")]
     return [f for f in files if os.path.isfile(f)]
 
 

@@ -96,12 +96,11 @@ __device__ __forceinline__ f32x2 pk_fma2(f32x2 w, f32x2 h, f32x2 acc) {
 
 // acc[r] += sum_k w[k] v[k][r] over k = 0..127: w as 64 register pairs, v in LDS as [k][R]
 // (broadcast reads: every lane of a wave reads the same address)
-template <int R>
+template <int R, int GK>
 __device__ __forceinline__ void lstm_matvec(const f32x2 (&w)[H / 2], const float* v, float (&acc)[R]) {
     // k in groups of GK; the LDS reads of group g + 1 are issued before group g's FMAs (a fence
     // between them keeps the compiler from hoisting all reads of the unrolled loop), so each
     // group's read latency hides behind the previous group's FMAs
-    constexpr int GK = R == 4 ? 4 : 8;       // k per group
     constexpr int NR = GK * R / 4;           // ds_read_b128 per group
     constexpr int NG = H / GK;
     f32x4v buf[2][NR];
@@ -168,14 +167,24 @@ __device__ __forceinline__ void lstm_matvec(const f32x2 (&w)[H / 2], const float
 // keep c in a register: gates i, f, g, o (PyTorch order) -> c, h; h goes to LDS for the next
 // step. Stores per (row, t): gates (post-activation) [B*T][512], c [B*T][128], h_{t-1}
 // [B*T][128] (the W_hh gradient's operand); h_T into cat[:, 0:128].
+// R < 4: waves 2R..7 carry no item; 2R of them are LOADERS that bring the rows' xp for step
+// t + 2 into a 3-slot LDS ring by LDS-DMA while step t runs (one 1-KiB piece each, issued
+// through inline asm so the compiler inserts no wait for it; the loader waits for its own piece
+// a step later, before the barrier that publishes it). No thread then waits on a global load
+// inside the recurrence: the old per-step xp load sat on the critical path, and since on gfx9
+// vmcnt also counts stores, the item waves' wait for it drained their stores too. Roles are
+// wave-uniform (readfirstlane): each wave branches past the other role's code.
 template <int R>
 __global__ __launch_bounds__(512) void lstm_fwd_reg_kernel(const float* __restrict__ xp, const float* __restrict__ whh,
                                                           int B, int T, float* __restrict__ gates,
                                                           float* __restrict__ cst, float* __restrict__ hprev,
                                                           float* __restrict__ cat) {
+    constexpr bool PF = R < 4;
     __shared__ __attribute__((aligned(16))) float hs[H * R];  // h_{t-1}, [k][r]
-    __shared__ __attribute__((aligned(16))) float gs[R * G];  // gate pre-activations, [r][n]
-    const int n = threadIdx.x;
+    __shared__ __attribute__((aligned(16))) float gs[R * G];  // gates (activated), [r][n]
+    __shared__ __attribute__((aligned(16))) float xs[PF ? 3 : 1][PF ? R * G : 4];  // xp ring, [slot][r][n]
+    const int n = threadIdx.x, lane = n & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(n >> 6);
     const int b0 = blockIdx.x * R;
     f32x2 w[H / 2];  // W_hh[n][k], k = 0..127, as register pairs
     {
@@ -187,41 +196,76 @@ __global__ __launch_bounds__(512) void lstm_fwd_reg_kernel(const float* __restri
             w[2 * k4 + 1] = f32x2{v.z, v.w};
         }
     }
-    const bool item = n < R * H;
+    const bool item = wave < 2 * R;  // == n < 128 R
+    const int gkind = wave >> 1;     // gate of column n: 0 i, 1 f, 2 g, 3 o
     const int ir = n / H, iu = n % H, irow = b0 + ir;
     const bool ivalid = item && irow < B;
+    // loader lw = wave - 2R < 2R moves the 1-KiB half (lw & 1) of row lw >> 1
+    const int lw = wave - 2 * R, lr = lw >> 1, lh = lw & 1;
+    const bool lact = PF && !item && lw < 2 * R && b0 + lr < B;
+    // piece source for step t: xsrc + t G; LDS: xl0 + slot (R G 4 bytes)
+    const float* xsrc = xp + (size_t)(b0 + lr) * T * G + 256 * lh + 4 * lane;
+    const uint32_t xl0 = lds_addr(&xs[0][lr * G + 256 * lh]);
+    auto xdma = [&](int t, int slot) { glds16(xsrc + (size_t)t * G, xl0 + slot * (R * G * 4)); };
     float c = 0.f, h = 0.f;
     if (n < R * H) hs[iu * R + ir] = 0.f;
+    if (lact) {
+        xdma(0, 0);
+        if (T > 1) xdma(1, 1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __syncthreads();
+    // this step's slot, rotated by pointer (an indexed xs[t % 3] read makes hipcc hoist the
+    // matvec's LDS reads far ahead of their FMAs and spill)
+    const float* xr = &xs[0][n];
+    int dslot = 2;  // the slot step t + 2 lands in
     for (int t = 0; t < T; ++t) {
         lstm_opaque(w);
         float acc[R];
+        if constexpr (PF) {
 #pragma unroll
-        for (int r = 0; r < R; ++r) acc[r] = b0 + r < B ? xp[((size_t)(b0 + r) * T + t) * G + n] : 0.f;
-        lstm_matvec<R>(w, hs, acc);
+            for (int r = 0; r < R; ++r) acc[r] = xr[r * G];
+        } else {
 #pragma unroll
-        for (int r = 0; r < R; ++r) gs[r * G + n] = acc[r];
-        __syncthreads();  // pre-activations visible; every thread is done reading hs for step t
+            for (int r = 0; r < R; ++r) acc[r] = b0 + r < B ? xp[((size_t)(b0 + r) * T + t) * G + n] : 0.f;
+        }
+        lstm_matvec<R, (R >= 2 ? 4 : 8)>(w, hs, acc);  // GK 8 at R = 2 spills here
+        if constexpr (PF) xr = t % 3 == 2 ? &xs[0][n] : xr + R * G;
+        // the gate's activation right here, on all 512 threads (gate kind n / 128 is wave-uniform),
+        // so the item phase between the two barriers only runs the cell update
+        if (gkind == 2) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) gs[r * G + n] = tanhf(acc[r]);
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r) gs[r * G + n] = sigm(acc[r]);
+        }
+        __syncthreads();  // gates visible; every thread is done reading hs and xs[t % 3]
         if (item) {
             const float* gp = gs + ir * G + iu;
-            const float ig = sigm(gp[0]), fg = sigm(gp[H]), gg = tanhf(gp[2 * H]), og = sigm(gp[3 * H]);
+            const float ig = gp[0], fg = gp[H], gg = gp[2 * H], og = gp[3 * H];
             const float hp = h;
             c = fg * c + ig * gg;
             h = og * tanhf(c);
             hs[iu * R + ir] = h;
             if (ivalid) {
-                const size_t e = (size_t)irow * T + t;
-                float* gr = gates + e * G + iu;
-                gr[0] = ig;
-                gr[H] = fg;
-                gr[2 * H] = gg;
-                gr[3 * H] = og;
+                // 32-bit element offsets (host-checked: B T 512 < 2^31): scalar base + one VGPR
+                const uint32_t e = (uint32_t)irow * T + t;
+                gates[e * G + iu] = ig;
+                gates[e * G + iu + H] = fg;
+                gates[e * G + iu + 2 * H] = gg;
+                gates[e * G + iu + 3 * H] = og;
                 cst[e * H + iu] = c;
                 hprev[e * H + iu] = hp;
-                if (t == T - 1) cat[(size_t)irow * CAT + iu] = h;
+                if (t == T - 1) cat[(uint32_t)irow * CAT + iu] = h;
             }
+        } else if (lact) {
+            // xp(t + 1) (issued at step t - 1) has landed; slot (t + 2) % 3 was last read at step t - 1
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (t + 2 < T) xdma(t + 2, dslot);
         }
-        __syncthreads();  // h_t visible for step t + 1; gs free again
+        dslot = dslot == 2 ? 0 : dslot + 1;
+        __syncthreads();  // h_t and xp(t + 1) visible for step t + 1; gs free again
     }
 }
 
@@ -232,21 +276,52 @@ __global__ __launch_bounds__(512) void lstm_fwd_reg_kernel(const float* __restri
 //   pre-activation grads (i, f, g, o) -> dG[B*T][512] (HBM) and dGs[512][R] (LDS); dc <- dc f
 // then every thread: part[q][r][u] = sum_j dGs[128 q + j][r] W_hh[128 q + j][u] (the four
 // quarter sums of dh_{t-1} = dgates W_hh, reduced by the item threads next step).
+// R < 4: the item threads read gates(t), c(t), c(t-1) from a 4-slot LDS ring that the loader
+// waves (2R..7) fill by LDS-DMA three steps ahead (pieces: per row two 1-KiB halves of the
+// gates and one 512-B c row), each loader waiting for its own pieces two steps later, before
+// the barrier that publishes them (see the forward kernel for why the storing waves must not
+// wait on loads).
 template <int R>
 __global__ __launch_bounds__(512) void lstm_bwd_reg_kernel(const float* __restrict__ gates, const float* __restrict__ cst,
                                                           const float* __restrict__ whh, const float* __restrict__ dcat,
                                                           int B, int T, float* __restrict__ dG) {
+    constexpr bool PF = R < 4;
+    constexpr int SLOT = R * (G + H);  // one step: gates [R][512] then c [R][128]
+    constexpr int NLW = 8 - 2 * R;     // loader waves
     __shared__ __attribute__((aligned(16))) float dGs[G * R];    // [n][r]
     __shared__ __attribute__((aligned(16))) float ps[4 * R * H];  // [q][r][u]
-    const int tid = threadIdx.x, q = tid / H, u = tid % H;
+    __shared__ __attribute__((aligned(16))) float ring[PF ? 4 : 1][PF ? SLOT : 4];
+    const int tid = threadIdx.x, q = tid / H, u = tid % H, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int b0 = blockIdx.x * R;
     f32x2 w[H / 2];  // W_hh[128 q + j][u], j = 0..127, as register pairs
 #pragma unroll
     for (int j = 0; j < H; j += 2)
         w[j / 2] = f32x2{whh[(size_t)(q * H + j) * H + u], whh[(size_t)(q * H + j + 1) * H + u]};
-    const bool item = tid < R * H;
+    const bool item = wave < 2 * R;  // == tid < 128 R
     const int ir = tid / H, irow = b0 + ir;  // item (ir, u)
     const bool ivalid = item && irow < B;
+    const bool lact = PF && !item;
+    const int lw = wave - 2 * R;
+    // piece pc (< 3R) of step t: row pc / 3; pc % 3 = 0, 1 -> gates half, 2 -> c (lanes < 32)
+    auto sdma = [&](int t) {
+        for (int pc = lw; pc < 3 * R; pc += NLW) {
+            const int r = pc / 3, k = pc - 3 * r;
+            if (b0 + r >= B) continue;
+            float* slot = ring[t & 3];
+            if (k < 2)
+                glds16(gates + ((size_t)(b0 + r) * T + t) * G + 256 * k + 4 * lane, lds_addr(slot + r * G + 256 * k));
+            else if (lane < 32)
+                glds16(cst + ((size_t)(b0 + r) * T + t) * H + 4 * lane, lds_addr(slot + R * G + r * H));
+        }
+    };
+    if (lact) {
+        sdma(T - 1);
+        if (T > 1) sdma(T - 2);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (T > 2) sdma(T - 3);
+    }
+    if constexpr (PF) __syncthreads();
     float dh = ivalid ? dcat[(size_t)irow * CAT + u] : 0.f, dc = 0.f;
     for (int t = T - 1; t >= 0; --t) {
         lstm_opaque(w);
@@ -256,10 +331,18 @@ __global__ __launch_bounds__(512) void lstm_bwd_reg_kernel(const float* __restri
             float dgi = 0.f, dgf = 0.f, dgg = 0.f, dgo = 0.f;
             if (ivalid) {
                 const size_t e = (size_t)irow * T + t;
-                const float* gr = gates + e * G + u;
-                const float ig = gr[0], fg = gr[H], gg = gr[2 * H], og = gr[3 * H];
-                const float ct = cst[e * H + u];
-                const float cp = t > 0 ? cst[(e - 1) * H + u] : 0.f;
+                float ig, fg, gg, og, ct, cp;
+                if constexpr (PF) {
+                    const float* gr = &ring[t & 3][ir * G + u];
+                    ig = gr[0], fg = gr[H], gg = gr[2 * H], og = gr[3 * H];
+                    ct = ring[t & 3][R * G + ir * H + u];
+                    cp = t > 0 ? ring[(t - 1) & 3][R * G + ir * H + u] : 0.f;
+                } else {
+                    const float* gr = gates + e * G + u;
+                    ig = gr[0], fg = gr[H], gg = gr[2 * H], og = gr[3 * H];
+                    ct = cst[e * H + u];
+                    cp = t > 0 ? cst[(e - 1) * H + u] : 0.f;
+                }
                 const float tc = tanhf(ct);
                 const float d_o = dh * tc;
                 dc += dh * og * (1.f - tc * tc);
@@ -279,12 +362,17 @@ __global__ __launch_bounds__(512) void lstm_bwd_reg_kernel(const float* __restri
             dGs[(H + u) * R + ir] = dgf;
             dGs[(2 * H + u) * R + ir] = dgg;
             dGs[(3 * H + u) * R + ir] = dgo;
+        } else if (lact) {
+            // step t - 2's pieces (issued at step t + 1) have landed; slot (t - 3) & 3 == (t + 1) & 3
+            // was last read at step t + 1 and, as c_{t-1}, at step t + 2
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (t >= 3) sdma(t - 3);
         }
-        __syncthreads();  // dgates visible; the item threads are done reading ps
+        __syncthreads();  // dgates and ring slot t - 2 visible; the item threads are done reading ps
         if (t > 0) {
             const float* dq = dGs + (size_t)q * H * R;
             float part[R] = {};
-            lstm_matvec<R>(w, dq, part);
+            lstm_matvec<R, (R == 4 ? 4 : 8)>(w, dq, part);
 #pragma unroll
             for (int r = 0; r < R; ++r) ps[(q * R + r) * H + u] = part[r];
         }
