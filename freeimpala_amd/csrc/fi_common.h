@@ -127,6 +127,21 @@ __device__ __forceinline__ void blds16(fi_i32x4 rsrc, uint32_t voff, uint32_t ld
         : "memory");
 }
 
+// blds16 with the non-temporal cache policy: for single-use streams (the V-trace inputs) the
+// line is not kept in the caches / Infinity Cache after it is read
+__device__ __forceinline__ void blds16_nt(fi_i32x4 rsrc, uint32_t voff, uint32_t lds_base) {
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %3\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %2, 0 offen nt lds\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(rsrc), "s"(lds_base)
+        : "memory");
+}
+
 // the same with 4 bytes per lane: LDS (lds_base + 4 * lane)
 __device__ __forceinline__ void blds4(fi_i32x4 rsrc, uint32_t voff, uint32_t lds_base) {
     uint32_t keep;

@@ -13,8 +13,9 @@
 // rows 8w..8w+7 of a chunk (lane = 8*row + column). Each chunk's pi/mu logits tiles
 // (32 rows x 8 columns x A floats) and the action/reward/discount/value tiles are
 // contiguous pieces of the (T,B,A)/(T,B) layouts and arrive by LDS-DMA
-// (buffer_load_dwordx4 ... lds) into a 2-slot ring (81,920 B at A=18, two workgroups per
-// CU); the next chunk is issued right after the landing barrier, with counted vmcnt waits.
+// (buffer_load_dwordx4 ... nt lds: read once, so not kept in the caches) into a 2-slot ring
+// (81,920 B at A=18, two workgroups per CU); the next chunk is issued right after the landing
+// barrier, with counted vmcnt waits.
 // Per element: packed-fp32 softmax statistics, one v_exp_f32 per logit. The reverse
 // recurrence acc_t = d_t + g_t c_t acc_{t+1} is an affine suffix scan: a 3-step butterfly
 // inside the wave (DPP row_ror:8, v_permlane16_swap, v_permlane32_swap: no LDS round trip),
@@ -261,7 +262,7 @@ __device__ __forceinline__ int vt_issue_chunk(const VtArgs& a, const VtRsrc& rs,
         const int t = max(t0 + tl, 0);
         // 32-bit buffer offsets (a (T, B, A) fp32 tensor is far below 4 GiB): no 64-bit
         // address arithmetic per piece
-        blds16(j < L::PT ? rs.pi : rs.mu, (uint32_t)((t * a.B + b0) * A * 4 + cb),
+        blds16_nt(j < L::PT ? rs.pi : rs.mu, (uint32_t)((t * a.B + b0) * A * 4 + cb),
                base + (j < L::PT ? 0 : L::LOGB) + jj * 1024);
         ++n;
     }
@@ -273,7 +274,7 @@ __device__ __forceinline__ int vt_issue_chunk(const VtArgs& a, const VtRsrc& rs,
         // the piece's 4/NW tiles come from up to 4 tensors: one descriptor per tile, lanes select
         const uint32_t off = (uint32_t)((t * a.B + b0) * 4 + (lane & 1) * 16);
         if constexpr (L::NW == 4) {
-            blds16(w == 0 ? rs.act : w == 1 ? rs.rew : w == 2 ? rs.disc : rs.val, off, base + L::SCO + w * 1024);
+            blds16_nt(w == 0 ? rs.act : w == 1 ? rs.rew : w == 2 ? rs.disc : rs.val, off, base + L::SCO + w * 1024);
         } else {
             const char* arr = s == 0 ? (const char*)a.act
                               : s == 1 ? (const char*)a.rew
