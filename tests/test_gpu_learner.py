@@ -403,3 +403,80 @@ def test_rejected_batch_under_comm_leaves_state_unchanged(orc, monkeypatch, atta
     np.testing.assert_array_equal(L.get_params(), R.get_params())
     L.close()
     R.close()
+
+
+def _two_devices():
+    from freeimpala_amd import hip
+    n = hip.device_count()
+    if n < 2:
+        pytest.skip(f"needs 2 GPUs (this box has {n}): RCCL refuses two ranks on one device")
+
+
+def test_two_device_data_parallel_matches_full_batch_and_oracle(orc):
+    """Batch-dim data parallelism on two devices (single process, fi_comm_init_all, one thread
+    per device as DeviceLearner::step_sharded runs it): each replica steps its half of the
+    batch, the in-step all-reduce sums the two shard gradients, so both replicas end with
+    identical parameters equal to one device stepping the whole batch, and to the oracle's
+    SGD step on the full batch (sum order across the shards differs: 1e-6 scaled). Skipped on
+    one-GPU boxes; kept ready for the first multi-GPU run."""
+    from concurrent.futures import ThreadPoolExecutor
+    from freeimpala_amd.learner import DeviceLearner, pack_records
+    _two_devices()
+    T, B = 4, 32
+    b = orc.synth_batch(51, T=T, B=B, A=18, D=128)
+    pk = lambda sl: pack_records(b["obs"][:, sl], b["mu"][:, sl], b["actions"][:, sl], b["rewards"][:, sl],
+                                 b["discounts"][:, sl], entry_size=T + 1)
+    halves = [slice(0, B // 2), slice(B // 2, B)]
+    full = mk(T=T, B=B, seed=6)
+    reps = [mk(T=T, B=B // 2, seed=6, device=d) for d in (0, 1)]
+    DeviceLearner.comm_init_all(reps)
+    assert [r.comm_info()["nranks"] for r in reps] == [2, 2]
+    p0 = full.get_params()
+    for r in reps:
+        np.testing.assert_array_equal(r.get_params(), p0)
+    st = full.step(pk(slice(None)))
+    with ThreadPoolExecutor(2) as ex:
+        res = list(ex.map(lambda i: reps[i].step(pk(halves[i])), (0, 1)))
+    np.testing.assert_array_equal(reps[0].get_params(), reps[1].get_params())
+    scaled_close(reps[0].get_params(), full.get_params(), 1e-6, "2-device vs 1-device params")
+    ref = oracle_step(orc, full, b, p0)
+    scaled_close(reps[0].get_params(), p0 - np.float32(1e-3) * ref["grads"], 1e-6, "2-device vs oracle SGD")
+    assert abs((res[0]["total_loss"] + res[1]["total_loss"]) - st["total_loss"]) <= 1e-5 * max(1, abs(st["total_loss"]))
+    for r in reps + [full]:
+        r.close()
+
+
+def test_two_device_reject_is_agreed(orc):
+    """A bad action in ONE replica's shard: the all-reduced reject flag makes BOTH replicas
+    skip the optimizer (both raise FI_ERR_INVALID, parameters and version unchanged on both), so
+    they stay identical. Skipped on one-GPU boxes."""
+    from concurrent.futures import ThreadPoolExecutor
+    from freeimpala_amd._abi import FiError
+    from freeimpala_amd.learner import DeviceLearner, pack_records
+    _two_devices()
+    T, B = 4, 16
+    good = orc.synth_batch(52, T=T, B=2 * B, A=18, D=128)
+    bad = {k: (None if v is None else v.copy()) for k, v in good.items()}
+    bad["actions"][1, B + 3] = 18  # in replica 1's half only
+    pk = lambda d, sl: pack_records(d["obs"][:, sl], d["mu"][:, sl], d["actions"][:, sl], d["rewards"][:, sl],
+                                    d["discounts"][:, sl], entry_size=T + 1)
+    halves = [slice(0, B), slice(B, 2 * B)]
+    reps = [mk(T=T, B=B, seed=9, optimizer="adam", device=d) for d in (0, 1)]
+    DeviceLearner.comm_init_all(reps)
+
+    def run(d, i):
+        try:
+            return reps[i].step(pk(d, halves[i]))
+        except FiError as e:
+            return e
+    with ThreadPoolExecutor(2) as ex:
+        list(ex.map(lambda i: run(good, i), (0, 1)))
+    p1 = [r.get_params() for r in reps]
+    with ThreadPoolExecutor(2) as ex:
+        out = list(ex.map(lambda i: run(bad, i), (0, 1)))
+    assert all(isinstance(o, FiError) for o in out), out
+    for r, p in zip(reps, p1):
+        np.testing.assert_array_equal(r.get_params(), p)
+    np.testing.assert_array_equal(reps[0].get_params(), reps[1].get_params())
+    for r in reps:
+        r.close()
