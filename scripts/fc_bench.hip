@@ -8,9 +8,11 @@
 #define FC_DG_CFG 224, 256, 1, 8, 64, 2, 1
 #define FC_WG_CFG 256, 224, 4, 2, 64, 2
 #include "../freeimpala_amd/csrc/fc_gemm.hip"
+#include "../freeimpala_amd/csrc/fc_blaslt.h"
 
 #include <cstdio>
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <string>
@@ -76,15 +78,17 @@ int main(int argc, char** argv) {
 #define WGV(nm, S, ...) add("wgrd " nm, 2, [&](hipStream_t st, int k) { return fc_wgrad_impl<__VA_ARGS__>(a3, dh, slab, dw[k], R, st, S); }, dw[0], dw[1], (size_t)FCK * FCO * 4)
     // the shipped configurations first (fc_gemm.hip FC_*_CFG), then alternatives
     FWDV("256x256 w4x2 bk64 ns2 prio", 256, 256, 4, 2, 64, 2, 1);
-    FWDV("256x256 w2x2 bk64 ns2 agpr", 256, 256, 2, 2, 64, 2, 4);
-    FWDV("256x256 w2x2 bk64 ns2 agpr prio", 256, 256, 2, 2, 64, 2, 5);
-    FWDV("256x256 w2x2 bk32 ns4 agpr", 256, 256, 2, 2, 32, 4, 4);
     DGV("224x256 w1x8 bk64 ns2 prio", 224, 256, 1, 8, 64, 2, 1);
-    DGV("224x256 w2x2 bk64 ns2 agpr", 224, 256, 2, 2, 64, 2, 4);
-    DGV("224x256 w1x4 bk64 ns2 agpr", 224, 256, 1, 4, 64, 2, 4);
-    DGV("224x256 w2x2 bk32 ns4 agpr", 224, 256, 2, 2, 32, 4, 4);
     WGV("256x224 w4x2 bk64 ns2", 9, 256, 224, 4, 2, 64, 2);
-    WGV("256x224 w4x2 bk32 ns4", 9, 256, 224, 4, 2, 32, 4);
+    // hipBLASLt (the default fwd / dgrad today), own output buffers: not bit-comparable
+    __bf16 *hb, *db;
+    CK(hipMalloc(&hb, (size_t)R * FCO * 2));
+    CK(hipMalloc(&db, (size_t)R * FCK * 2));
+    FcBlasLt* F = std::getenv("FCB_NO_BLASLT") ? nullptr : fc_blaslt_create(R, a3, w, dh, hb, db, s);
+    if (F) {
+        add("fwd  hipBLASLt", 3, [&](hipStream_t st, int) { return fc_blaslt_forward(F, a3, w, bias, hb, st); }, hb, hb, 0);
+        add("dgrd hipBLASLt", 4, [&](hipStream_t st, int) { return fc_blaslt_dgrad(F, dh, w, db, st); }, db, db, 0);
+    }
     std::vector<std::vector<float>> ms(vs.size());
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
