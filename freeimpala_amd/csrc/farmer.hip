@@ -523,14 +523,24 @@ static int splits_for(int M) { return std::max(1, std::min(16, M / 256)); }
 
 // weight gradient [N][K] of a layer (PyTorch layout) + its bias gradient, deterministic
 static int wgrad(fi_farmer* f, const float* dY, int M, int N, const float* X, int ldx, int K, float* gW, float* gb) {
+    // one split: the GEMM / column sum write the gradient itself (a one-slab reduce is a copy;
+    // at small batches these extra launches are a quarter of the step's dispatches)
     const int sp = splits_for(M);
     FI_REQUIRE((size_t)sp * N * K <= f->slab_floats, "farmer: slab too small");
-    FI_TRY(f32_gemm_tn_wgrad(dY, M, N, X, ldx, K, sp, f->slab, f->stream));
-    FI_TRY(reduce_slabs(f->slab, sp, (size_t)N * K, gW, f->stream));
+    if (sp == 1) {
+        FI_TRY(f32_gemm_tn_wgrad(dY, M, N, X, ldx, K, 1, gW, f->stream));
+    } else {
+        FI_TRY(f32_gemm_tn_wgrad(dY, M, N, X, ldx, K, sp, f->slab, f->stream));
+        FI_TRY(reduce_slabs(f->slab, sp, (size_t)N * K, gW, f->stream));
+    }
     if (gb) {
         const int cs = std::max(1, std::min(64, M / 64));
-        FI_TRY(colsum_partial(dY, M, N, cs, f->slab, f->stream));
-        FI_TRY(reduce_slabs(f->slab, cs, (size_t)N, gb, f->stream));
+        if (cs == 1) {
+            FI_TRY(colsum_partial(dY, M, N, 1, gb, f->stream));
+        } else {
+            FI_TRY(colsum_partial(dY, M, N, cs, f->slab, f->stream));
+            FI_TRY(reduce_slabs(f->slab, cs, (size_t)N, gb, f->stream));
+        }
     }
     return FI_OK;
 }
