@@ -79,6 +79,11 @@ int main(int argc, char** argv) {
     // the shipped configurations first (fc_gemm.hip FC_*_CFG), then alternatives
     FWDV("256x256 w4x2 bk64 ns2 prio", 256, 256, 4, 2, 64, 2, 1);
     DGV("224x256 w1x8 bk64 ns2 prio", 224, 256, 1, 8, 64, 2, 1);
+    DGV("224x256 w2x4 bk64 ns2 prio", 224, 256, 2, 4, 64, 2, 1);
+    DGV("224x256 w2x4 bk64 ns2", 224, 256, 2, 4, 64, 2, 0);
+    DGV("224x256 w2x4 bk32 ns4 prio", 224, 256, 2, 4, 32, 4, 1);
+    DGV("448x128 w4x2 bk64 ns2 prio", 448, 128, 4, 2, 64, 2, 1);
+    DGV("224x128 w2x4 bk64 ns2 prio", 224, 128, 2, 4, 64, 2, 1);
     WGV("256x224 w4x2 bk64 ns2", 9, 256, 224, 4, 2, 64, 2);
     // hipBLASLt (the default fwd / dgrad today), own output buffers: not bit-comparable
     __bf16 *hb, *db;
