@@ -822,6 +822,19 @@ AtariNet* atari_create(int B, int T, int A) {
             return nullptr;
         }
     }
+    // the data-gradient rows T*B.. (dh, da3, da2, da1) are never written by the backward (it walks
+    // T*B frames): zeros, so those tensors read as the exact gradients (0) there -- after the
+    // library's algorithm timing, which fills dh with test data -- on the creation stream and
+    // waited for (no legacy-stream memset racing the learner's stream)
+    if (hipMemsetAsync(I->dh, 0, N * 512 * sizeof(__bf16), s0) != hipSuccess ||
+        hipMemsetAsync(I->da3, 0, N * 3136 * sizeof(__bf16), s0) != hipSuccess ||
+        hipMemsetAsync(I->da2, 0, N * 81 * 64 * sizeof(__bf16), s0) != hipSuccess ||
+        hipMemsetAsync(I->da1, 0, N * 400 * 32 * sizeof(__bf16), s0) != hipSuccess || hipStreamSynchronize(s0) != hipSuccess) {
+        set_error("atari: hipMemsetAsync failed");
+        (void)hipStreamDestroy(s0);
+        atari_destroy(n);
+        return nullptr;
+    }
     (void)hipStreamDestroy(s0);
     return n;
 }
@@ -893,6 +906,11 @@ int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, con
                    float* grads, hipStream_t s, KernelTagger* tg, GradReadyHook* gr) {
     AtariImpl* I = impl(n);
     const int N = I->N, A = I->A, O = A + 1;
+    // the last B frames (t = T) only give the bootstrap value: their dlogits do not exist and
+    // their dvalue is 0, so every gradient they would add is exactly 0 -- the frame-resident
+    // backward kernels walk the first T*B frames only (dh rows T*B.. stay the zeros written at
+    // creation, for the library fc dgrad that reads all N rows)
+    const int Nb = I->TB;
     const Offsets& o = I->off;
     using namespace geo;
     float* slab = I->slab;
@@ -902,11 +920,11 @@ int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, con
 #define FI_A(tag, x) do { TagScope ts_(tg, tag); rc = (x); if (rc) return rc; } while (0)
     // heads: wgrad [512][O] + bias, dgrad -> dh (masked by h)
     if (O == 19) {  // packed-fp32 VALU kernels (A = 18, the configured action set)
-        FI_A("heads_wgrad", heads_wgrad_launch(dlogits, dvalue, I->h, slab, cs, N, I->TB, s));
+        FI_A("heads_wgrad", heads_wgrad_launch(dlogits, dvalue, I->h, slab, cs, Nb, I->TB, s));
         FI_A("reduce_slabs", reduce_slabs(slab, kHeadsGrid, (size_t)FCO * O, grads + o.hw, s));
         FI_A("reduce_slabs", reduce_slabs(cs, kHeadsGrid, (size_t)O, grads + o.hb, s));
         // heads dgrad also leaves the fc bias partials (column sums of dh) in the slab
-        FI_A("heads_dgrad", heads_dgrad_launch(dlogits, dvalue, I->params + o.hw, I->h, I->dh, N, I->TB, slab, s));
+        FI_A("heads_dgrad", heads_dgrad_launch(dlogits, dvalue, I->params + o.hw, I->h, I->dh, Nb, I->TB, slab, s));
         FI_A("reduce_slabs", reduce_slabs(slab, kHeadsDgradGrid, (size_t)FCO, grads + o.fcb, s));
     } else {
         FI_A("heads_wgrad", (wgrad<128, 32, 4, 1>(RowsBf16{I->h, N, FCO}, dout, slab, cs, N, FCO, O, SPL_H, 1.f, s)));
@@ -921,16 +939,16 @@ int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, con
     // fc: wgrad (fc_gemm.hip) as fp32 slabs reduced into the gradient blob, bias = column
     // sums of dh (left by heads dgrad), dgrad -> da3 unmasked (conv3's backward applies the
     // a3 ReLU mask as it loads da3)
-    FI_A("fc_wgrad", fc_wgrad_launch(I->a3, I->dh, slab, grads + o.fcw, N, s));
+    FI_A("fc_wgrad", fc_wgrad_launch(I->a3, I->dh, slab, grads + o.fcw, Nb, s));
     // buckets in reverse layer order: fc + heads (95 % of the gradient bytes) reduce while
     // fc dgrad, conv3 and conv2/conv1 backward run
     if (gr && (rc = gr->ready(o.fcw, o.total - o.fcw))) return rc;
     FI_A("fc_dgrad", I->fc ? fc_blaslt_dgrad(I->fc, I->dh, I->wb.fcB, I->da3, s)
-                           : fc_dgrad_launch(I->dh, I->wb.fcB, I->da3, N, s));
+                           : fc_dgrad_launch(I->dh, I->wb.fcB, I->da3, I->fr ? Nb : N, s));  // the GEMM path reads all N
     // conv3: wgrad [576][64] + bias, dgrad -> da2 (masked by a2)
     if (I->fr) {
         const int grid = std::min(N, I->fr_grid);
-        FI_A("conv3_bwd", conv3_bwd_fr_launch(I->a2, I->da3, I->a3, I->wb.c3D, I->da2, slab, cs, N, grid, s));
+        FI_A("conv3_bwd", conv3_bwd_fr_launch(I->a2, I->da3, I->a3, I->wb.c3D, I->da2, slab, cs, Nb, grid, s));
         FI_A("reduce_slabs", reduce_slabs(slab, grid, (size_t)C3K * C3O, grads + o.c3w, s));
         FI_A("reduce_slabs", reduce_slabs(cs, grid, (size_t)C3O, grads + o.c3b, s));
         if (gr && (rc = gr->ready(o.c3w, o.fcw - o.c3w))) return rc;
@@ -951,7 +969,7 @@ int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, con
         float* slab1 = slab + (size_t)grid * C2K * C2O;
         float* cs1 = cs + (size_t)grid * C2O;
         FI_A("conv21_bwd", conv21_bwd_fr_launch(I->a1, I->da2, I->wb.c2D, frames, I->keep_da1 ? I->da1 : nullptr,
-                                                slab, cs, slab1, cs1, N, grid, s, I->a1_planar));
+                                                slab, cs, slab1, cs1, Nb, grid, s, I->a1_planar));
         FI_A("reduce_slabs", reduce_slabs(slab, grid, (size_t)C2K * C2O, grads + o.c2w, s));
         FI_A("reduce_slabs", reduce_slabs(cs, grid, (size_t)C2O, grads + o.c2b, s));
         FI_A("reduce_slabs", reduce_slabs(slab1, grid, (size_t)C1K * C1O, grads + o.c1w, s));
@@ -962,7 +980,7 @@ int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, con
     // conv2: wgrad [512][64] + bias, dgrad -> da1 (4 parity classes, masked by a1)
     if (I->fr) {
         const int grid = std::min(N, I->fr_grid);
-        FI_A("conv2_bwd", conv2_bwd_fr_launch(I->a1, I->da2, I->wb.c2D, I->da1, slab, cs, N, grid, s));
+        FI_A("conv2_bwd", conv2_bwd_fr_launch(I->a1, I->da2, I->wb.c2D, I->da1, slab, cs, Nb, grid, s));
         FI_A("reduce_slabs", reduce_slabs(slab, grid, (size_t)C2K * C2O, grads + o.c2w, s));
         FI_A("reduce_slabs", reduce_slabs(cs, grid, (size_t)C2O, grads + o.c2b, s));
     } else {
@@ -977,7 +995,7 @@ int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, con
     // conv1: wgrad [256][32] (+1/255 input scale) + bias
     if (I->fr) {
         const int grid = std::min(N, I->fr_grid);
-        FI_A("conv1_wgrad", conv1_wgrad_fr_launch(frames, I->da1, slab, cs, N, grid, s));
+        FI_A("conv1_wgrad", conv1_wgrad_fr_launch(frames, I->da1, slab, cs, Nb, grid, s));
         FI_A("reduce_slabs", reduce_slabs(slab, grid, (size_t)C1K * C1O, grads + o.c1w, s));
         FI_A("reduce_slabs", reduce_slabs(cs, grid, (size_t)C1O, grads + o.c1b, s));
     } else {
