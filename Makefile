@@ -59,11 +59,17 @@ host: build/mpi_pool_check
 # the reference tree is read in place, never copied; the binary travels to the GPU box)
 REF ?= /root/reference
 ifneq ($(wildcard $(REF)/include/freeimpala/data_structures.h),)
-host: build/reference_binding
+host: build/reference_binding build/reference_mpi_check
 endif
 build/reference_binding: tests/cpp/reference_binding.cpp tests/cpp/stubs/spdlog/spdlog.h $(wildcard include/freeimpala_amd/*.hpp) include/fi_learner.h $(LIBDIR)/libfi_learner.so
 	@mkdir -p build
 	g++ -std=c++17 -O2 -Wall -I$(REF)/include -Itests/cpp/stubs -Iinclude -include optional $< -o $@ -L$(LIBDIR) -lfi_learner -pthread '-Wl,-rpath,$$ORIGIN/../$(LIBDIR)' -Wl,-rpath,/opt/rocm/lib
+
+# INTEGRATION.md section 3b's rank-0 patch (mpi::LearnerEndpoint) on the reference's own
+# SharedBuffer / ModelManager, its Agent on the actor ranks, and the section 2 alias learner
+build/reference_mpi_check: tests/cpp/reference_mpi_check.cpp tests/cpp/stubs/spdlog/spdlog.h $(wildcard include/freeimpala_amd/*.hpp) include/fi_learner.h $(LIBDIR)/libfi_learner.so
+	@mkdir -p build
+	g++ -std=c++17 -O2 -Wall -I$(REF)/include -Itests/cpp/stubs -Iinclude -I$(MPI_HOME)/include -include optional $< -o $@ -L$(LIBDIR) -lfi_learner -pthread '-Wl,-rpath,$$ORIGIN/../$(LIBDIR)' -Wl,-rpath,/opt/rocm/lib $(MPI_LINK)
 
 clean:
 	rm -rf build $(LIBDIR)

@@ -132,7 +132,7 @@ public:
             shared_buffers_.push_back(std::make_shared<Buffer>(entry_size_, buffer_capacity_));
     }
 
-    ~BasicLearner() { stop(); }
+    virtual ~BasicLearner() { stop(); }
     BasicLearner(const BasicLearner&) = delete;
     BasicLearner& operator=(const BasicLearner&) = delete;
 
@@ -194,7 +194,16 @@ public:
     size_t param_bytes() const { return device_->param_bytes(); }
     const LearnerConfig& config() const { return cfg_; }
     size_t learnerTimeMs() const { return train_time_ms_; }  // accepted; the device step replaces the sleep
-    bool workerFailed() const { return worker_failed_.load(); }  // a worker ended on a device failure
+    // A worker ended on a device failure. Its buffer is then draining: blocked readers and (on
+    // buffer types whose write honours draining, freeimpala_amd::SharedBuffer) blocked writers
+    // return, so callers poll this flag instead of waiting for iterations that never come.
+    bool workerFailed() const { return worker_failed_.load(); }
+
+protected:
+    // fi_learner_acquire_staging for the zero-copy worker path; virtual so a test can make it fail
+    virtual int acquireStaging(fi_learner* h, void** dst, size_t* stride) {
+        return fi_learner_acquire_staging(h, dst, stride);
+    }
 
 private:
     void workerThread(size_t player_index) {
@@ -235,10 +244,11 @@ private:
         fi_learner* h = device_->handle(p);
         void* dst = nullptr;
         size_t stride = 0;
-        if (fi_learner_acquire_staging(h, &dst, &stride) != FI_OK) {
+        if (acquireStaging(h, &dst, &stride) != FI_OK) {
             log("error", "player " + std::to_string(p) + ": acquire_staging failed, worker stops: " +
                              fi_last_error());
             worker_failed_.store(true);
+            shared_buffers_[p]->setDraining();  // wake this player's readers and writers
             return -1;
         }
         if (!shared_buffers_[p]->readBatchInto(batch_size_, static_cast<char*>(dst), stride)) return 0;

@@ -41,12 +41,25 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <type_traits>
+#include <utility>
 #include <vector>
 
 #include "freeimpala_amd/replay.hpp"
 
 namespace freeimpala_amd {
 namespace mpi {
+
+namespace detail {
+// Buffer::write(const char*, size_t) (freeimpala_amd::SharedBuffer) is used when the buffer type
+// has it; the reference SharedBuffer only has write(const std::vector<char>&)
+// (data_structures.h:219), which gets the received vector trimmed to the message size.
+template <class B, class = void>
+struct has_write_ptr : std::false_type {};
+template <class B>
+struct has_write_ptr<B, std::void_t<decltype(std::declval<B&>().write((const char*)nullptr, size_t{}))>>
+    : std::true_type {};
+}  // namespace detail
 
 struct EndpointStats {
     uint64_t trajectories = 0, trajectory_bytes = 0, version_requests = 0, weights_replies = 0,
@@ -156,8 +169,17 @@ private:
         MPI_Irecv(b.data(), (int)b.size(), MPI_BYTE, MPI_ANY_SOURCE, MPI_ANY_TAG, comm_, &r);
     }
     void recycle(std::vector<char>&& b) {
+        b.resize(slot_bytes_);  // a vector trimmed for Buffer::write regrows within its capacity
         std::lock_guard<std::mutex> lk(pool_mu_);
         if (pool_.size() < (size_t)n_slots_) pool_.push_back(std::move(b));
+    }
+    bool write_entry(Buffer& buf, Msg& m) {
+        if constexpr (detail::has_write_ptr<Buffer>::value) {
+            return buf.write(m.data.data(), m.bytes);
+        } else {  // the reference's write(const std::vector<char>&): exactly the received bytes
+            m.data.resize(m.bytes);
+            return buf.write(static_cast<const std::vector<char>&>(m.data));
+        }
     }
     void enqueue(Msg&& m) {
         {
@@ -214,7 +236,7 @@ private:
             return bump(&EndpointStats::bad_messages);
         }
         // blocks while the buffer is full (the reference's write, mpi_async_pool/main.cpp:260)
-        if (!bufs_[p]->write(m.data.data(), m.bytes)) return bump(&EndpointStats::dropped_entries);
+        if (!write_entry(*bufs_[p], m)) return bump(&EndpointStats::dropped_entries);
         std::lock_guard<std::mutex> lk(smu_);
         ++stats_.trajectories;
         stats_.trajectory_bytes += m.bytes;

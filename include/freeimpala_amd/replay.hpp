@@ -70,11 +70,15 @@ public:
         not_full_.notify_all();
     }
 
-    // Blocking enqueue; false when the data is larger than an entry.
+    // Blocking enqueue; false when the data is larger than an entry, or when the buffer is
+    // full and draining. The reference's write waits for space even while draining
+    // (data_structures.h:223), so a writer on a full buffer whose reader has stopped blocks
+    // forever; here setDraining releases it (a learner worker that fails drains its buffer).
     bool write(const std::vector<char>& data) { return write(data.data(), data.size()); }
     bool write(const char* data, size_t n) {
         std::unique_lock<std::mutex> lk(mu_);
-        not_full_.wait(lk, [this] { return count_ < capacity_; });
+        not_full_.wait(lk, [this] { return count_ < capacity_ || draining_.load(); });
+        if (count_ >= capacity_) return false;
         return push_locked(lk, data, n);
     }
 

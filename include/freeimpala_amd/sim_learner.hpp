@@ -77,6 +77,7 @@ public:
     std::vector<std::shared_ptr<Buffer>> getSharedBuffers() { return shared_buffers_; }
     std::shared_ptr<Manager> getModelManager() { return model_manager_; }
     size_t iterations(size_t p) const { return iterations_.at(p).load(); }
+    bool workerFailed() const { return false; }  // no device: nothing fails
     const LearnerConfig& config() const { return cfg_; }
     size_t param_bytes() const { return kModelBytes; }
 

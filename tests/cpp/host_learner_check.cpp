@@ -10,6 +10,12 @@
 //       record schema) from the same parameters; checks the two results are identical,
 //       then writes the batch, the parameters and the step statistics to OUT_DIR so that
 //       tests/test_host_cpp.py can compare them with the CPU oracle.
+//   host_learner_check worker_fail DIR
+//       freeimpala_amd::Learner whose staging acquisition fails (a test subclass): the worker
+//       must stop, report workerFailed(), and drain its buffer so an actor blocked in write() on
+//       the full buffer returns instead of hanging.
+#include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -20,6 +26,7 @@
 #include <vector>
 
 #include "freeimpala_amd/device_learner.hpp"
+#include "freeimpala_amd/learner.hpp"
 
 using freeimpala_amd::DeviceLearner;
 using freeimpala_amd::LearnerConfig;
@@ -188,11 +195,48 @@ static int gpu_mode(const std::string& out) {
     return 0;
 }
 
+struct FailingLearner : freeimpala_amd::Learner {
+    using freeimpala_amd::Learner::Learner;
+    std::atomic<int> calls{0};
+    int acquireStaging(fi_learner*, void**, size_t*) override {
+        ++calls;
+        return FI_ERR_STATE;
+    }
+};
+
+static int worker_fail_mode(const std::string& dir) {
+    LearnerConfig c;
+    c.seq_length = 8;
+    constexpr size_t CAP = 4, S = 9, M = 2, WRITES = 3 * CAP;
+    FailingLearner L(1, CAP, S, M, 0, 0, dir, "", 100, c);
+    L.start();
+    auto buf = L.getSharedBuffers()[0];
+    std::atomic<int> written{0}, refused{0};
+    std::atomic<bool> done{false};
+    std::thread agent([&] {  // more entries than the buffer holds: blocks once it is full
+        const std::vector<char> e(S * FI_RECORD_BYTES, 1);
+        for (size_t i = 0; i < WRITES; ++i) (buf->write(e) ? written : refused)++;
+        done = true;
+    });
+    for (int i = 0; i < 3000 && !done; ++i) std::this_thread::sleep_for(std::chrono::milliseconds(10));
+    if (!done) {
+        std::fprintf(stderr, "actor still blocked in write() after the worker failed\n");
+        std::_Exit(1);  // the blocked thread cannot be joined
+    }
+    agent.join();
+    CHECK(L.workerFailed() && L.iterations(0) == 0 && L.calls.load() == 1);
+    CHECK(refused.load() > 0 && (size_t)(written.load() + refused.load()) == WRITES);
+    L.stop();
+    std::printf("OK worker_fail written=%d refused=%d\n", written.load(), refused.load());
+    return 0;
+}
+
 int main(int argc, char** argv) {
     const std::string mode = argc > 1 ? argv[1] : "cpu";
     try {
         if (mode == "cpu") return cpu_mode();
         if (mode == "gpu" && argc > 2) return gpu_mode(argv[2]);
+        if (mode == "worker_fail" && argc > 2) return worker_fail_mode(argv[2]);
     } catch (const std::exception& e) {
         std::fprintf(stderr, "unexpected exception: %s\n", e.what());
         return 1;

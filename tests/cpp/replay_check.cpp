@@ -76,6 +76,18 @@ static int buffer_checks() {
     CHECK(sb3.readBatch(1)[0] == entry(1024, 9));
     w.join();
     CHECK(wrote && sb3.readBatch(1)[0] == entry(1024, 10));
+    // a writer blocked on a full buffer is released by setDraining with false (the learner's
+    // worker drains its buffer when it fails, so actors do not hang on it); a draining buffer
+    // with space still takes entries
+    SharedBuffer sb4(1, 1);
+    CHECK(sb4.write(entry(1024, 11)));
+    bool wrote4 = true;
+    std::thread w4([&] { wrote4 = sb4.write(entry(1024, 12)); });
+    std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    sb4.setDraining();
+    w4.join();
+    CHECK(!wrote4 && sb4.getFilledCount() == 1);
+    CHECK(sb4.readBatch(1)[0] == entry(1024, 11) && sb4.write(entry(1024, 13)) && sb4.getFilledCount() == 1);
     return 0;
 }
 

@@ -73,3 +73,13 @@ def test_host_cpp_two_players_vs_oracle(orc, tmp_path):
     l2 = np.linalg.norm(g_dev - g) / np.linalg.norm(g)
     assert l2 < 2e-3, l2  # recovered through an fp32 parameter difference
     np.testing.assert_allclose(st["grad_norm"], np.linalg.norm(g.astype(np.float64)), rtol=1e-4)
+
+
+@pytest.mark.gpu
+def test_worker_failure_drains_buffer_and_releases_actors(tmp_path):
+    """a worker whose staging acquisition fails stops, reports workerFailed(), and
+    drains its buffer, so an actor blocked in SharedBuffer::write returns (false) instead of
+    hanging the run."""
+    r = subprocess.run([_build(), "worker_fail", str(tmp_path)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "OK worker_fail" in r.stdout

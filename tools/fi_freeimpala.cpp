@@ -106,7 +106,7 @@ int run(const Params& P, const LearnerConfig& lc, const std::string& kind) {
     // stops right away, main.cpp:241-242, which makes its iteration count timing-dependent)
     const auto t_wait = std::chrono::steady_clock::now();
     for (size_t p = 0; p < P.num_players; ++p)
-        while (learner->iterations(p) < learner_iterations &&
+        while (learner->iterations(p) < learner_iterations && !learner->workerFailed() &&
                std::chrono::steady_clock::now() - t_wait < std::chrono::minutes(10))
             std::this_thread::sleep_for(std::chrono::milliseconds(1));
     const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -125,6 +125,10 @@ int run(const Params& P, const LearnerConfig& lc, const std::string& kind) {
     report(P, "{\"learner\": \"" + kind + "\", \"learner_iterations\": " + iterations_json(*learner, P.num_players) +
                   ", \"expected_iterations\": " + std::to_string(learner_iterations) + ", \"param_bytes\": " +
                   std::to_string(learner->param_bytes()) + buf + ", \"metrics\": " + metrics->summaryJson() + "}");
+    if (learner->workerFailed()) {  // a worker stopped on a device failure: the run is incomplete
+        std::cerr << "learner: a worker stopped on a device failure\n";
+        return 5;
+    }
     return 0;
 }
 

@@ -81,7 +81,7 @@ int run_learner(int world, const Params& P, const LearnerConfig& lc) {
     // every actor is done and every entry written: wait for the workers to consume them
     // (floor(A * iterations / M) steps per player), then stop (drain + final save)
     for (size_t p = 0; p < P.num_players; ++p)
-        while (learner->iterations(p) < learner_iterations &&
+        while (learner->iterations(p) < learner_iterations && !learner->workerFailed() &&
                std::chrono::steady_clock::now() - t0 < std::chrono::minutes(10))
             std::this_thread::sleep_for(std::chrono::milliseconds(1));
     const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -106,6 +106,10 @@ int run_learner(int world, const Params& P, const LearnerConfig& lc) {
                   ", \"expected_iterations\": " + std::to_string(learner_iterations) + ", \"param_bytes\": " +
                   std::to_string(learner->device().param_bytes()) + ", \"mpi\": " + buf +
                   ", \"metrics\": " + metrics->summaryJson() + "}");
+    if (learner->workerFailed()) {  // a worker stopped on a device failure: the run is incomplete
+        std::cerr << "learner: a worker stopped on a device failure\n";
+        return 5;
+    }
     return 0;
 }
 
