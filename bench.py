@@ -305,9 +305,9 @@ def load_counters(arch, tba):
     """(traffic, mfma, info) from the newest profiles/*pmc_{traffic,mfma}_<arch>*.json whose
     _build.source_hash matches this tree; empty dicts when none does."""
     import glob
-    from freeimpala_amd.build_info import source_hash
-    h = source_hash()
-    info = {"source_hash": h, "traffic_file": None, "mfma_file": None}
+    from freeimpala_amd.build_info import runtime_key, source_hash
+    h, rt = source_hash(), runtime_key()
+    info = {"source_hash": h, "runtime": rt, "traffic_file": None, "mfma_file": None}
     if tba != (100, 4096, 18):
         return {}, {}, dict(info, note="counter passes exist for T=100 B=4096 A=18 only")
 
@@ -318,14 +318,15 @@ def load_counters(arch, tba):
                     d = json.load(fh)
             except (OSError, ValueError):
                 continue
-            if d.get("_build", {}).get("source_hash") == h:
+            b = d.get("_build", {})
+            if b.get("source_hash") == h and b.get("runtime") == rt:  # same kernels, same switches
                 return os.path.relpath(f, ROOT), {k: v for k, v in d.items() if not k.startswith("_")}
         return None, {}
 
     info["traffic_file"], tr = newest("traffic")
     info["mfma_file"], mf = newest("mfma")
     if not info["traffic_file"] and not info["mfma_file"]:
-        info["note"] = "no counter pass stamped with this source hash: traffic / mfma_util_pmc null"
+        info["note"] = "no counter pass stamped with this source hash and runtime: traffic / mfma_util_pmc null"
     return {k: v["hbm_bytes_per_launch"] for k, v in tr.items()}, mf, info
 
 

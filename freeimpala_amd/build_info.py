@@ -33,9 +33,30 @@ def source_hash() -> str:
     return h.hexdigest()[:16]
 
 
+# run-time switches that change which kernels the learner step launches, or how: a counter pass
+# taken under one setting says nothing about a bench line timed under another
+KERNEL_ENV = ("FI_FR_GRID", "FI_FC_OWN", "FI_BLT_NO_SWEEP", "FI_KEEP_DA1", "FI_BWD_UNFUSED", "FI_FWD_UNFUSED",
+              "FI_A1_NHWC", "FI_ATARI_GENERIC", "FI_DETERMINISTIC")
+
+
+def rocm_version() -> str:
+    for p in ("/opt/rocm/.info/version", "/opt/rocm/.info/version-dev"):
+        try:
+            with open(p) as fh:
+                return fh.read().strip()
+        except OSError:
+            pass
+    return "unknown"
+
+
+def runtime_key() -> dict:
+    """The kernel-relevant FI_* environment (set ones only) and the ROCm release."""
+    return {"env": {k: os.environ[k] for k in KERNEL_ENV if k in os.environ}, "rocm": rocm_version()}
+
+
 def stamp(extra=None) -> dict:
     """The `_build` object a counter summary carries."""
-    d = {"source_hash": source_hash()}
+    d = {"source_hash": source_hash(), "runtime": runtime_key()}
     if extra:
         d.update(extra)
     return d

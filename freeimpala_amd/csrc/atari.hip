@@ -751,7 +751,7 @@ int conv21_bwd_fr_launch(const __bf16* a1, const __bf16* da2, const __bf16* w2d,
 int conv2_bwd_fr_launch(const __bf16* a1, const __bf16* da2, const __bf16* w2d, __bf16* da1, float* slab,
                         float* cs_slab, int nframes, int grid, hipStream_t s);
 int conv3_bwd_fr_launch(const __bf16* a2, const __bf16* da3, const __bf16* a3, const __bf16* w3d, __bf16* da2,
-                        float* slab, float* cs_slab, int nframes, int grid, hipStream_t s);
+                        float* slab, float* cs_slab, float* cs2, int nframes, int grid, hipStream_t s);
 
 static AtariImpl* impl(AtariNet* n) { return (AtariImpl*)n->impl; }
 
@@ -948,7 +948,10 @@ int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, con
     // conv3: wgrad [576][64] + bias, dgrad -> da2 (masked by a2)
     if (I->fr) {
         const int grid = std::min(N, I->fr_grid);
-        FI_A("conv3_bwd", conv3_bwd_fr_launch(I->a2, I->da3, I->a3, I->wb.c3D, I->da2, slab, cs, Nb, grid, s));
+        // conv2's bias partials ([grid][2][64] at cs + 3 grid 64, past c3b [grid][64] and
+        // c1b [grid][4][32]) come from conv3_bwd (FI_C2B_C3) or from conv21_bwd
+        FI_A("conv3_bwd", conv3_bwd_fr_launch(I->a2, I->da3, I->a3, I->wb.c3D, I->da2, slab, cs, cs + (size_t)3 * grid * C2O,
+                                              Nb, grid, s));
         FI_A("reduce_slabs", reduce_slabs(slab, grid, (size_t)C3K * C3O, grads + o.c3w, s));
         FI_A("reduce_slabs", reduce_slabs(cs, grid, (size_t)C3O, grads + o.c3b, s));
         if (gr && (rc = gr->ready(o.c3w, o.fcw - o.c3w))) return rc;
@@ -969,9 +972,9 @@ int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, con
         float* slab1 = slab + (size_t)grid * C2K * C2O;
         float* cs1 = cs + (size_t)grid * C2O;
         FI_A("conv21_bwd", conv21_bwd_fr_launch(I->a1, I->da2, I->wb.c2D, frames, I->keep_da1 ? I->da1 : nullptr,
-                                                slab, cs, slab1, cs1, Nb, grid, s, I->a1_planar));
+                                                slab, cs + (size_t)3 * grid * C2O, slab1, cs1, Nb, grid, s, I->a1_planar));
         FI_A("reduce_slabs", reduce_slabs(slab, grid, (size_t)C2K * C2O, grads + o.c2w, s));
-        FI_A("reduce_slabs", reduce_slabs(cs, grid, (size_t)C2O, grads + o.c2b, s));
+        FI_A("reduce_slabs", reduce_slabs(cs + (size_t)3 * grid * C2O, 2 * grid, (size_t)C2O, grads + o.c2b, s));
         FI_A("reduce_slabs", reduce_slabs(slab1, grid, (size_t)C1K * C1O, grads + o.c1w, s));
         FI_A("reduce_slabs", reduce_slabs(cs1, 4 * grid, (size_t)C1O, grads + o.c1b, s));
         if (gr && (rc = gr->ready(0, o.c3w))) return rc;
@@ -980,9 +983,11 @@ int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, con
     // conv2: wgrad [512][64] + bias, dgrad -> da1 (4 parity classes, masked by a1)
     if (I->fr) {
         const int grid = std::min(N, I->fr_grid);
-        FI_A("conv2_bwd", conv2_bwd_fr_launch(I->a1, I->da2, I->wb.c2D, I->da1, slab, cs, Nb, grid, s));
+        FI_A("conv2_bwd", conv2_bwd_fr_launch(I->a1, I->da2, I->wb.c2D, I->da1, slab, cs + (size_t)3 * grid * C2O, Nb,
+                                              grid, s));
         FI_A("reduce_slabs", reduce_slabs(slab, grid, (size_t)C2K * C2O, grads + o.c2w, s));
-        FI_A("reduce_slabs", reduce_slabs(cs, grid, (size_t)C2O, grads + o.c2b, s));
+        // the bias partials in the fused path's layout and place (bit-identical gradients)
+        FI_A("reduce_slabs", reduce_slabs(cs + (size_t)3 * grid * C2O, 2 * grid, (size_t)C2O, grads + o.c2b, s));
     } else {
         FI_A("conv2_wgrad", (wgrad<128, 64, 2, 2>(ConvGather<20, 32, 4, 2, 9>{I->a1, N * P2}, RowsBf16{I->da2, N * P2, C2O},
                                slab, cs, N * P2, C2K, C2O, SPL_C2, 1.f, s)));

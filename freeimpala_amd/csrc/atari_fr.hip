@@ -121,6 +121,22 @@ constexpr int IMG = 2 * PLANE;                      // 56,576 B
 constexpr int OUT = 400 * 32 * 2;                   // 25,600 B output / dY tile
 }  // namespace c1
 
+// Where the bias sums go (A/B switches; the layout of the partials is the same either way):
+//   FI_C2B_C3   conv2's bias partials summed by conv3_bwd's data-gradient epilogue (from the da2
+//               it stores) instead of by conv21's weight-gradient waves (48 v_dot2 per frame)
+//   FI_C1B_PH2  conv1's bias partials from the B fragments of conv1's weight gradient in phase 2
+//               (m-steps split over the four waves at compile time) instead of the phase-1
+//               epilogue (16 VALU per tile)
+//   FI_C21_PKMASK  the da1 ReLU mask per 32-bit word (relu_mask_pair) instead of per element
+#ifndef FI_C2B_C3
+#define FI_C2B_C3 0
+#endif
+#ifndef FI_C1B_PH2
+#define FI_C1B_PH2 1
+#endif
+#ifndef FI_C21_PKMASK
+#define FI_C21_PKMASK 1
+#endif
 // sum of a fragment's 8 bf16 values into acc: 4 v_dot2c_f32_bf16 against (1, 1) instead of 8
 // conversions + 8 adds (the weight-gradient waves' bias column sums of dY)
 __device__ __forceinline__ float sum8_bf16(const bf16x8& v, float acc) {
@@ -131,6 +147,20 @@ __device__ __forceinline__ float sum8_bf16(const bf16x8& v, float acc) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_fdot2_f32_bf16(pv.p[j], one, acc, false);
     return acc;
+}
+
+// bf16 pair {bf16(a), bf16(b)} with each half zeroed where the matching s16 half of `mask` is
+// not > 0 (ReLU derivative of a stored bf16 activation; -0 and negatives count as off):
+// 0 - m with signed saturation is negative exactly for m > 0, its arithmetic shift by 15 the
+// half-word mask
+__device__ __forceinline__ uint32_t relu_mask_pair(float a, float b, uint32_t mask) {
+    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+    const bf16x2 v = {(__bf16)a, (__bf16)b};
+    // (the shift count comes from a register: an inline constant of a packed instruction feeds
+    // its high half from the constant's upper 16 bits, i.e. 0 for 15)
+    uint32_t t;
+    asm("v_pk_sub_i16 %0, 0, %1 clamp\n\tv_pk_ashrrev_i16 %0, %2, %0" : "=&v"(t) : "v"(mask), "v"(0x000F000Fu));
+    return __builtin_bit_cast(uint32_t, v) & t;
 }
 
 __device__ __forceinline__ void u8x16_to_bf16(u32x4 v, bf16x8& lo, bf16x8& hi) {
@@ -1200,11 +1230,17 @@ __global__ __launch_bounds__(512, 2) void conv2_bwd_fr(const __bf16* __restrict_
                     const int k = 128 * wr + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
                     out[k * 64 + 32 * ct + col] = accw[t][ct][r];
                 }
-        if (wr == 0) {  // lanes l and l+32 hold the same co (16*(g&1) + (l&15)), other m half
+        // lanes l and l+32 hold the same co (16*(g&1) + (l&15)), other m half; cs_slab has the
+        // [grid][2][64] layout of conv21_bwd_fr's (row 1 zero), unless conv3_bwd fills it (FI_C2B_C3)
+        if (!FI_C2B_C3 && wr == 0) {
             const float o0 = __shfl_xor(bsum0, 32, 64), o1 = __shfl_xor(bsum1, 32, 64);
+            float* cb = cs_slab + (size_t)blockIdx.x * 128;
             if (lane < 32) {
-                cs_slab[(size_t)blockIdx.x * 64 + lane] = bsum0 + o0;
-                cs_slab[(size_t)blockIdx.x * 64 + 32 + lane] = bsum1 + o1;
+                cb[lane] = bsum0 + o0;
+                cb[32 + lane] = bsum1 + o1;
+            } else {
+                cb[64 + lane - 32] = 0.f;
+                cb[96 + lane - 32] = 0.f;
             }
         }
     } else {
@@ -1337,9 +1373,9 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                                                         const uint8_t* __restrict__ frames,
                                                         __bf16* __restrict__ da1_out,  // optional (parity checks)
                                                         float* __restrict__ slab2,     // [grid][512][64]
-                                                        float* __restrict__ cs2,       // [grid][64]
+                                                        float* __restrict__ cs2,       // [grid][2][64] (unless FI_C2B_C3)
                                                         float* __restrict__ slab1,     // [grid][256][32]
-                                                        float* __restrict__ cs1,       // [grid][4 classes][32]
+                                                        float* __restrict__ cs1,       // [grid][4 waves][32]
                                                         int nframes, int a1_planar) {
     __shared__ __attribute__((aligned(16))) char smem[c21::LDS];
     const int lane = threadIdx.x & 63, tid = threadIdx.x;
@@ -1381,7 +1417,11 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
     const int dc = 2 * (g & 1) + (p4 >> 1);
     const int db0 = dsw(8 * (g >> 1) + q, dc) + 8 * (p4 & 1), db1 = dsw(8 * (g >> 1) + q + 4, dc) + 8 * (p4 & 1);
     f32x16 acc1[2] = {};
-    auto conv1_wgrad = [&]() {
+    // conv1's bias gradient = column sums of da1: the B fragment of m-step ms holds 8 pixels of
+    // channel lane & 31, so wave 4 + wr sums the fragments of m-steps ms = wr (mod 4) beside its
+    // MFMAs (4 v_dot2 in a 64-cycle MFMA pair) instead of 16 VALU per tile in the phase-1 epilogue
+    float bsum1 = 0.f;
+    auto conv1_wgrad = [&](auto wrc) {  // wrc: wr as a compile-time constant (the bias split)
         // im2col offset of lane row m = 16ms + m0 (m0 = 8(g>>1) + q + 4hh < 16): output pixel
         // (oy, ox) = divmod(m, 20), input pixel (4oy + ky, 4ox + kx) with kx = 4(g&1) + p4, so
         // offset = base + 16 (m + 64 oy); with 16ms = 20a + b (compile time), oy = a + [m0 >= 20 - b]
@@ -1414,6 +1454,9 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
 #pragma unroll
             for (int kt = 0; kt < 2; ++kt)
                 acc1[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[1 + kt], cur[0], acc1[kt], 0, 0, 0);
+            if constexpr (FI_C1B_PH2) {
+                if ((ms & 3) == decltype(wrc)::value) bsum1 = sum8_bf16(cur[0], bsum1);
+            }
         }
     };
 
@@ -1500,8 +1543,10 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                 for (int ms = 0; ms < 6; ++ms) {
                     const bf16x8* cur = fb[ms & 1];
                     if (ms + 1 < 6) load(ms + 1, fb[(ms + 1) & 1]);
-                    bsum0 = sum8_bf16(cur[0], bsum0);
-                    bsum1_ = sum8_bf16(cur[1], bsum1_);
+                    if constexpr (!FI_C2B_C3) {
+                        bsum0 = sum8_bf16(cur[0], bsum0);
+                        bsum1_ = sum8_bf16(cur[1], bsum1_);
+                    }
 #pragma unroll
                     for (int t = 0; t < 4; ++t) {
                         accw[t][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[2 + t], cur[0], accw[t][0], 0, 0, 0);
@@ -1558,11 +1603,17 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                     const int k = 128 * wr + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
                     out[k * 64 + 32 * ct + col] = accw[t][ct][r];
                 }
-        if (wr == 0) {
-            const float o0 = __shfl_xor(bsum0, 32, 64), o1 = __shfl_xor(bsum1_, 32, 64);
-            if (lane < 32) {
-                cs2[(size_t)blockIdx.x * 64 + lane] = bsum0 + o0;
-                cs2[(size_t)blockIdx.x * 64 + 32 + lane] = bsum1_ + o1;
+        if constexpr (!FI_C2B_C3) {  // cs2[block][0][64] (row [1] zero: the layout conv3_bwd fills otherwise)
+            if (wr == 0) {
+                const float o0 = __shfl_xor(bsum0, 32, 64), o1 = __shfl_xor(bsum1_, 32, 64);
+                float* cb = cs2 + (size_t)blockIdx.x * 128;
+                if (lane < 32) {
+                    cb[lane] = bsum0 + o0;
+                    cb[32 + lane] = bsum1_ + o1;
+                } else {
+                    cb[64 + lane - 32] = 0.f;
+                    cb[96 + lane - 32] = 0.f;
+                }
             }
         }
     } else {
@@ -1591,7 +1642,7 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
         const int si = (lane & 15) ^ (((lane & 15) >> 1) & 4);
         const int bd0 = 16 * (si + 128 * g + c2::zc(g));
         const int bd6 = 16 * (min(96 + si, 99) + 128 * g + c2::zc(g));
-        float bs8[8] = {};  // conv1 bias partials: channels 8g + j of this lane's da1 pixels
+        float bs8[8] = {};  // !FI_C1B_PH2: conv1 bias partials, channels 8g + j of this lane's da1 pixels
         PH_DECL
         for (int it = 0; it < nmine; ++it) {
             const int f = frame_of(it);
@@ -1617,22 +1668,34 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                 auto mask_of = [&](int pt) {
                     return *(const s16x8*)(X + 64 * (100 * wr + min(pt * 16 + si, 99)) + 16 * g);
                 };
-                // tile pt's epilogue: mask by (a1 > 0), into D (and da1_out), conv1 bias partials
+                // tile pt's epilogue: mask by (a1 > 0), into D (and da1_out): the bf16 pairs and
+                // the mask are handled per 32-bit word (3 packed ops per pair instead of two
+                // compares, two selects and the repacking)
                 auto epilogue = [&](int pt, const f32x4& e0, const f32x4& e1, const s16x8& m) {
                     const int ri = pt * 16 + si;
                     if (pt < 6 || ri < 100) {
                         const int iyq = ri / 10, ixq = ri - 10 * iyq;
                         const int pix = (2 * iyq + ty) * 20 + 2 * ixq + tx;
-                        bf16x8 o;
+                        u32x4 ov;
+                        if constexpr (FI_C21_PKMASK) {
+                            const u32x4 mw = __builtin_bit_cast(u32x4, m);
+                            ov = u32x4{relu_mask_pair(e0[0], e0[1], mw[0]), relu_mask_pair(e0[2], e0[3], mw[1]),
+                                       relu_mask_pair(e1[0], e1[1], mw[2]), relu_mask_pair(e1[2], e1[3], mw[3])};
+                        } else {
+                            bf16x8 o;
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            o[r] = m[r] > 0 ? (__bf16)e0[r] : (__bf16)0.f;
-                            o[4 + r] = m[4 + r] > 0 ? (__bf16)e1[r] : (__bf16)0.f;
+                            for (int r = 0; r < 4; ++r) {
+                                o[r] = m[r] > 0 ? (__bf16)e0[r] : (__bf16)0.f;
+                                o[4 + r] = m[4 + r] > 0 ? (__bf16)e1[r] : (__bf16)0.f;
+                            }
+                            ov = __builtin_bit_cast(u32x4, o);
                         }
-                        const u32x4 ov = __builtin_bit_cast(u32x4, o);
                         *(u32x4*)(D + dsw(pix, g)) = ov;
+                        if constexpr (!FI_C1B_PH2) {
+                            const bf16x8 o = __builtin_bit_cast(bf16x8, ov);
 #pragma unroll
-                        for (int j = 0; j < 8; ++j) bs8[j] += (float)o[j];
+                            for (int j = 0; j < 8; ++j) bs8[j] += (float)o[j];
+                        }
                         if constexpr (KEEP_DA1) FI_ST16(ov, dst + 4 * pix + g);
                     }
                 };
@@ -1673,19 +1736,30 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
             lds_barrier();  // B2: D and the image complete
             PH(1);
             if (it + 1 < nmine) load_raw(it + 1);
-            conv1_wgrad();
+            switch (wr) {  // the bias split is compile-time per wave (no branch in the m-step loop)
+                case 0: conv1_wgrad(std::integral_constant<int, 0>{}); break;
+                case 1: conv1_wgrad(std::integral_constant<int, 1>{}); break;
+                case 2: conv1_wgrad(std::integral_constant<int, 2>{}); break;
+                default: conv1_wgrad(std::integral_constant<int, 3>{}); break;
+            }
             PH(3);
             PH_ITER();
         }
         PH_FLUSH();
-        // conv1 bias partial of this class wave: sum over the 16 lanes of each channel group
+        // conv1 bias partial of this wave: channel lane & 31, the two pixel halves of the B
+        // fragments combined
+        if constexpr (FI_C1B_PH2) {
+            const float other = __shfl_xor(bsum1, 32, 64);
+            if (lane < 32) cs1[((size_t)blockIdx.x * 4 + wr) * 32 + lane] = bsum1 + other;
+        } else {  // sum over the 16 lanes of each channel group
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
+            for (int j = 0; j < 8; ++j)
 #pragma unroll
-            for (int o = 1; o < 16; o <<= 1) bs8[j] += __shfl_xor(bs8[j], o, 64);
-        if ((lane & 15) == 0) {
+                for (int o = 1; o < 16; o <<= 1) bs8[j] += __shfl_xor(bs8[j], o, 64);
+            if ((lane & 15) == 0) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) cs1[((size_t)blockIdx.x * 4 + wr) * 32 + 8 * g + j] = bs8[j];
+                for (int j = 0; j < 8; ++j) cs1[((size_t)blockIdx.x * 4 + wr) * 32 + 8 * g + j] = bs8[j];
+            }
         }
     }
     if (w >= 4) {  // conv1 weight-gradient slab rows k = 32(2wr + kt) + (r&3) + 8(r>>2) + 4(lane>>5)
@@ -1965,6 +2039,7 @@ __global__ __launch_bounds__(512, 2) void conv3_bwd_fr(const __bf16* __restrict_
                                                        __bf16* __restrict__ da2,
                                                        float* __restrict__ slab,     // [grid][576][64]
                                                        float* __restrict__ cs_slab,  // [grid][64]
+                                                       float* __restrict__ cs2,      // [grid][2][64] conv2 bias partials
                                                        int nframes) {
     __shared__ __attribute__((aligned(16))) char smem[c3::LDS];
     const int lane = threadIdx.x & 63;
@@ -1991,6 +2066,10 @@ __global__ __launch_bounds__(512, 2) void conv3_bwd_fr(const __bf16* __restrict_
             }
         const int si = (lane & 15) ^ (((lane & 15) >> 1) & 4);
         const int cg = g;  // dY chunk of k-step ks: g + 4(ks&1)
+        // conv2's bias gradient is the column sum of da2 as stored (masked, bf16): summed here,
+        // where the values are in registers anyway, instead of by conv21's weight-gradient waves
+        // (48 v_dot2 per frame beside their MFMAs); channels 8c + j of this lane's pixels
+        float bs8[8] = {};  // FI_C2B_C3 only
         // Tap skipping: dX pixel (iy, ix) meets dY row iy - ky, which exists only for
         // 0 <= iy - ky <= 6 (the zero border supplies the rest). Pixel tiles are 16 pixels of
         // the 9-wide image, so tile 0 (rows 0-1) never needs kernel row 2, tile 4 (rows 7-8)
@@ -2049,6 +2128,10 @@ __global__ __launch_bounds__(512, 2) void conv3_bwd_fr(const __bf16* __restrict_
                         o[4 + r] = m[4 + r] > 0 ? (__bf16)acc[ti][1][r] : (__bf16)0.f;
                     }
                     FI_ST16(__builtin_bit_cast(u32x4, o), dst + 8 * ri + c);
+                    if constexpr (FI_C2B_C3) {
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) bs8[j] += (float)o[j];
+                    }
                 }
             }
         };
@@ -2056,13 +2139,25 @@ __global__ __launch_bounds__(512, 2) void conv3_bwd_fr(const __bf16* __restrict_
             if (ph) work(std::integral_constant<int, 1>{}, X, f);
             else work(std::integral_constant<int, 0>{}, X, f);
         });
+        // sum over the 16 lanes (pixels) of each channel group; wave (chh, ph) owns channels
+        // 32chh..+32 of its pixel tiles -> cs2[block][ph][64]
+        if constexpr (FI_C2B_C3) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) bs8[j] += __shfl_xor(bs8[j], o, 64);
+            if ((lane & 15) == 0) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) cs2[((size_t)blockIdx.x * 2 + ph) * 64 + 8 * (4 * chh + g) + j] = bs8[j];
+            }
+        }
     }
 }
 
 int conv3_bwd_fr_launch(const __bf16* a2, const __bf16* da3, const __bf16* a3, const __bf16* w3d, __bf16* da2,
-                        float* slab, float* cs_slab, int nframes, int grid, hipStream_t s) {
+                        float* slab, float* cs_slab, float* cs2, int nframes, int grid, hipStream_t s) {
     hipLaunchKernelGGL(conv3_bwd_fr, dim3(grid), dim3(512), 0, s, a2, da3, a3, w3d, da2,
-                       slab, cs_slab, nframes);
+                       slab, cs_slab, cs2, nframes);
     FI_HIP_CHECK(hipGetLastError());
     st_report("conv3_bwd");
     ph_report("conv3_bwd", grid);

@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -37,7 +38,7 @@ constexpr int IN = 162, H = 128, G = 4 * H, XD = 484, CAT = H + XD, DW = 512;
 
 struct Off {
     size_t wih, whh, bih, bhh, w[7], b[7], total;
-    Off() {
+    __host__ __device__ Off() {
         size_t o = 0;
         wih = o; o += (size_t)G * IN;
         whh = o; o += (size_t)G * H;
@@ -450,6 +451,282 @@ __global__ __launch_bounds__(DW) void head_bwd_kernel(const float* __restrict__ 
     if (k == 0) *gb6 = sb;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Small-batch torso (B <= 64, the reference's default B = 32): the five 512-wide layers and the
+// head in ONE launch per direction instead of ~6 (forward) / ~22 (backward) small GEMM /
+// column-sum / head launches, each of which ran a long K loop on a handful of workgroups.
+// 128 workgroups (co-resident: one per CU at most) x 256 threads; workgroup w owns the four
+// columns 4w..4w+3 of every layer (forward: output features; backward: the rows of each weight
+// gradient and the matching columns of each data gradient). Layers are separated by a grid
+// barrier (cdna_hip_programming.md Guideline 16: every storing wave drains, one lane releases
+// at agent scope and adds to a monotone counter, polls it relaxed, acquires; bounded spin with a
+// status word). fp32 VALU throughout (the fp32 MFMA rate equals the vector rate on gfx950).
+//   tile  out[b][c] = sum_k X[b][k] S[k][c], c < 4: thread (row r = t & 31 (+32), k-group
+//         t >> 5) accumulates its k range (float4 loads of its X row, broadcast LDS reads of
+//         S[k][0..3]); the eight k-group partials are summed in a fixed order (deterministic).
+// Layer 1's X is the virtual concat (h_T | x): cat[:, 0:128] from the recurrence, x itself for
+// the rest (no copy kernel).
+constexpr int SM_WG = DW / 4;  // 128 workgroups
+constexpr int SM_MAXB = 64;
+
+struct SmSync {
+    unsigned* cnt;     // monotone arrival counter (host supplies the base of this launch)
+    unsigned* status;  // nonzero: a barrier gave up
+    unsigned base;
+};
+
+// all waves of the workgroup: returns false when the barrier timed out (then every workgroup
+// stops; the host reports the status word)
+__device__ __forceinline__ bool sm_grid_sync(const SmSync& sy, unsigned phase, int* lds_flag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(sy.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned target = sy.base + phase * (unsigned)gridDim.x;
+        int ok = 1;
+        for (unsigned spins = 0; (int)(__hip_atomic_load(sy.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0;) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins > (1u << 22)) {
+                __hip_atomic_fetch_or(sy.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = 0;
+                break;
+            }
+        }
+        if (ok && __hip_atomic_load(sy.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) ok = 0;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        *lds_flag = ok;
+    }
+    __syncthreads();
+    return *lds_flag != 0;
+}
+
+// X row r (< B) as float4 at k (k % 4 == 0): plain rows of pitch K, or layer 1's concat
+struct SmRows {
+    const float* a;  // rows of pitch lda (cat when `x` is set: columns 0..127)
+    int lda;
+    const float* x;  // layer 1: x [B][484] supplies columns 128..611
+    __device__ f32x4v load(int r, int k) const {
+        if (x && k >= H) return *(const f32x4v*)(x + (size_t)r * XD + (k - H));
+        return *(const f32x4v*)(a + (size_t)r * lda + k);
+    }
+};
+
+// S[k][0..3] in LDS (K rows) x X -> part[kg][r][c]; then thread t < 4B: r = t >> 2, c = t & 3,
+// returns the fixed-order sum of the eight k-group partials (0 for t >= 4B)
+template <int RPT>
+__device__ __forceinline__ float sm_tile(const SmRows& X, int B, int K, const f32x4v* S, f32x4v* part) {
+    const int t = threadIdx.x, kg = t >> 5, r0 = t & 31;
+    const int KC = (K + 31) / 32 * 4, k0 = kg * KC, k1 = min(K, k0 + KC);
+    f32x2 acc[RPT][2];
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) acc[q][0] = acc[q][1] = f32x2{0.f, 0.f};
+    for (int k = k0; k < k1; k += 4) {
+        const f32x4v s0 = S[k], s1 = S[k + 1], s2 = S[k + 2], s3 = S[k + 3];
+#pragma unroll
+        for (int q = 0; q < RPT; ++q) {
+            const int r = r0 + 32 * q;
+            const f32x4v xv = r < B ? X.load(r, k) : f32x4v{0.f, 0.f, 0.f, 0.f};
+            acc[q][0] = pk_fma2(f32x2{s0.x, s0.y}, f32x2{xv.x, xv.x}, acc[q][0]);
+            acc[q][1] = pk_fma2(f32x2{s0.z, s0.w}, f32x2{xv.x, xv.x}, acc[q][1]);
+            acc[q][0] = pk_fma2(f32x2{s1.x, s1.y}, f32x2{xv.y, xv.y}, acc[q][0]);
+            acc[q][1] = pk_fma2(f32x2{s1.z, s1.w}, f32x2{xv.y, xv.y}, acc[q][1]);
+            acc[q][0] = pk_fma2(f32x2{s2.x, s2.y}, f32x2{xv.z, xv.z}, acc[q][0]);
+            acc[q][1] = pk_fma2(f32x2{s2.z, s2.w}, f32x2{xv.z, xv.z}, acc[q][1]);
+            acc[q][0] = pk_fma2(f32x2{s3.x, s3.y}, f32x2{xv.w, xv.w}, acc[q][0]);
+            acc[q][1] = pk_fma2(f32x2{s3.z, s3.w}, f32x2{xv.w, xv.w}, acc[q][1]);
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < RPT; ++q)
+        part[kg * SM_MAXB + r0 + 32 * q] = f32x4v{acc[q][0].x, acc[q][0].y, acc[q][1].x, acc[q][1].y};
+    __syncthreads();
+    float v = 0.f;
+    if (t < 4 * B) {
+        const int r = t >> 2, c = t & 3;
+#pragma unroll
+        for (int g = 0; g < 8; ++g) v += part[g * SM_MAXB + r][c];
+    }
+    return v;
+}
+
+// S[k][c] = W[c0 + c][k] (four rows of a [out][K] weight: the forward's operand)
+__device__ __forceinline__ void sm_load_rows(const float* W, int K, int c0, f32x4v* S) {
+    float* Sf = (float*)S;
+    for (int i = threadIdx.x; i < 4 * K; i += blockDim.x) {
+        const int c = i / K, k = i - c * K;
+        Sf[4 * k + c] = W[(size_t)(c0 + c) * K + k];
+    }
+}
+// S[j][i] = W[j][c0 + i], j < 512 (four columns of a [512][Kin] weight: the data gradient's)
+__device__ __forceinline__ void sm_load_cols(const float* W, int Kin, int c0, f32x4v* S) {
+    for (int j = threadIdx.x; j < DW; j += blockDim.x) S[j] = *(const f32x4v*)(W + (size_t)j * Kin + c0);
+}
+
+struct SmFwdArgs {
+    const float* P;  // parameters (Off layout)
+    const float* cat;
+    const float* x;
+    float* act[6];
+    float* val;
+    int B;
+    SmSync sy;
+};
+
+template <int RPT>
+__global__ __launch_bounds__(256) void mlp_fwd_small_kernel(SmFwdArgs a) {
+    __shared__ f32x4v S[CAT];
+    __shared__ f32x4v part[8 * SM_MAXB];
+    __shared__ int flag;
+    const Off o;
+    const int c0 = 4 * blockIdx.x, t = threadIdx.x, B = a.B;
+    for (int l = 1; l <= 5; ++l) {
+        const int K = l == 1 ? CAT : DW;
+        sm_load_rows(a.P + o.w[l], K, c0, S);
+        __syncthreads();
+        const SmRows X = l == 1 ? SmRows{a.cat, CAT, a.x} : SmRows{a.act[l - 1], DW, nullptr};
+        const float v = sm_tile<RPT>(X, B, K, S, part);
+        if (t < 4 * B) {
+            const int r = t >> 2, c = t & 3;
+            a.act[l][(size_t)r * DW + c0 + c] = fmaxf(v + a.P[o.b[l] + c0 + c], 0.f);
+        }
+        if (!sm_grid_sync(a.sy, l, &flag)) return;
+    }
+    // head (dense6): value[b] = act5[b] . w6 + b6, one wave per row, on workgroup 0
+    if (blockIdx.x != 0) return;
+    const int lane = t & 63;
+    for (int r = t >> 6; r < B; r += 4) {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < DW / 64; ++i) s = fmaf(a.act[5][(size_t)r * DW + lane + 64 * i], a.P[o.w[6] + lane + 64 * i], s);
+        s = wave_sum(s);
+        if (lane == 0) a.val[r] = s + a.P[o.b[6]];
+    }
+}
+
+struct SmBwdArgs {
+    const float* P;
+    float* Gd;  // gradient blob (Off layout)
+    const float* cat;
+    const float* x;
+    const float* act[6];
+    const float* val;
+    const float* y;
+    float* dval;
+    double* loss;
+    float* dY[2];  // ping-pong [B][512] data gradients of the layer outputs
+    float* dcat;   // [B][CAT], columns 0..127 written
+    int B, kind;
+    SmSync sy;
+};
+
+// the criterion's gradient for row b (loss_kernel's formulas)
+__device__ __forceinline__ float sm_dval(float v, float yv, int kind, float invn, float* l) {
+    const float d = v - yv, ad = fabsf(d);
+    if (kind == FI_LOSS_MSE) {
+        *l = d * d;
+        return (2.0f * invn) * d;
+    }
+    if (kind == FI_LOSS_MAE) {
+        *l = ad;
+        return (d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f)) * invn;
+    }
+    *l = ad < 1.f ? 0.5f * d * d : ad - 0.5f;
+    return (d < -1.f ? -1.f : (d > 1.f ? 1.f : d)) * invn;
+}
+
+// weight-gradient rows c0..c0+3 of a [512][K] weight: gW[c0 + i][k] = sum_b dy[b][i] X[b][k]
+// (b in order), bias gb[c0 + i] = sum_b dy[b][i]; dy [B][4] in LDS
+__device__ __forceinline__ void sm_wgrad(const float* dy4, const SmRows& X, int B, int K, int c0, float* gW, float* gb) {
+    const f32x4v* dy = (const f32x4v*)dy4;
+    for (int k = threadIdx.x; k < K; k += blockDim.x) {
+        f32x4v acc = {0.f, 0.f, 0.f, 0.f};
+        const float* col = X.x && k >= H ? X.x + (k - H) : X.a + k;
+        const int ld = X.x && k >= H ? XD : X.lda;
+        for (int b = 0; b < B; ++b) acc += dy[b] * col[(size_t)b * ld];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) gW[(size_t)(c0 + i) * K + k] = acc[i];
+    }
+    if (threadIdx.x < 4) {
+        float sb = 0.f;
+        for (int b = 0; b < B; ++b) sb += dy4[4 * b + threadIdx.x];
+        gb[c0 + threadIdx.x] = sb;
+    }
+}
+
+template <int RPT>
+__global__ __launch_bounds__(256) void mlp_bwd_small_kernel(SmBwdArgs a) {
+    __shared__ f32x4v S[DW];
+    __shared__ f32x4v part[8 * SM_MAXB];
+    __shared__ float dy4[4 * SM_MAXB];
+    __shared__ float dv[SM_MAXB];
+    __shared__ int flag;
+    const Off o;
+    const int c0 = 4 * blockIdx.x, t = threadIdx.x, B = a.B;
+    // criterion gradient, every workgroup for itself (B values); workgroup 0 also the loss
+    const float invn = 1.0f / (float)B;
+    if (t < B) {
+        float l;
+        dv[t] = sm_dval(a.val[t], a.y[t], a.kind, invn, &l);
+        if (blockIdx.x == 0) a.dval[t] = dv[t];
+    }
+    __syncthreads();
+    if (blockIdx.x == 0 && t == 0) {
+        double s = 0.0;
+        for (int b = 0; b < B; ++b) {
+            float l;
+            sm_dval(a.val[b], a.y[b], a.kind, invn, &l);
+            s += (double)l;
+        }
+        *a.loss = s / (double)B;
+        float sb = 0.f;
+        for (int b = 0; b < B; ++b) sb += dv[b];
+        a.Gd[o.b[6]] = sb;
+    }
+    // dense6 backward on this workgroup's columns: gw6, and dY5 = (act5 > 0) dval w6
+    if (t < 4 * B) {
+        const int r = t >> 2, c = t & 3, k = c0 + c;
+        const float av = a.act[5][(size_t)r * DW + k];
+        const float d = av > 0.f ? dv[r] * a.P[o.w[6] + k] : 0.f;
+        dy4[t] = d;
+        a.dY[0][(size_t)r * DW + k] = d;
+    }
+    if (t < 4) {
+        float s = 0.f;
+        for (int b = 0; b < B; ++b) s = fmaf(dv[b], a.act[5][(size_t)b * DW + c0 + t], s);
+        a.Gd[o.w[6] + c0 + t] = s;
+    }
+    __syncthreads();
+    sm_wgrad(dy4, SmRows{a.act[4], DW, nullptr}, B, DW, c0, a.Gd + o.w[5], a.Gd + o.b[5]);
+    if (!sm_grid_sync(a.sy, 1, &flag)) return;
+    // layer l's data gradient -> dY of layer l-1 (ReLU-masked), then layer l-1's weight gradient
+    for (int l = 5; l >= 2; --l) {
+        const float* dyl = a.dY[(5 - l) & 1];
+        float* dyn = a.dY[(5 - l + 1) & 1];
+        sm_load_cols(a.P + o.w[l], DW, c0, S);
+        __syncthreads();
+        const float v = sm_tile<RPT>(SmRows{dyl, DW, nullptr}, B, DW, S, part);
+        if (t < 4 * B) {
+            const int r = t >> 2, c = t & 3, k = c0 + c;
+            const float d = a.act[l - 1][(size_t)r * DW + k] > 0.f ? v : 0.f;
+            dy4[t] = d;
+            dyn[(size_t)r * DW + k] = d;
+        }
+        __syncthreads();
+        const SmRows X = l - 1 == 1 ? SmRows{a.cat, CAT, a.x} : SmRows{a.act[l - 2], DW, nullptr};
+        sm_wgrad(dy4, X, B, l - 1 == 1 ? CAT : DW, c0, a.Gd + o.w[l - 1], a.Gd + o.b[l - 1]);
+        if (!sm_grid_sync(a.sy, 7 - l, &flag)) return;
+    }
+    // dcat[:, 0:128] = dY1 . W1[:, 0:128] (the recurrence's upstream gradient): workgroups 0..31
+    if (c0 >= H) return;
+    sm_load_cols(a.P + o.w[1], CAT, c0, S);
+    __syncthreads();
+    const float v = sm_tile<RPT>(SmRows{a.dY[0], DW, nullptr}, B, DW, S, part);
+    if (t < 4 * B) a.dcat[(size_t)(t >> 2) * CAT + c0 + (t & 3)] = v;
+}
+
 // b_ih and b_hh receive the same gradient (column sums of dG)
 __global__ void copy_kernel(const float* __restrict__ src, float* __restrict__ dst, int n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -504,6 +781,9 @@ struct fi_farmer {
     double* loss = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     hipEvent_t pe[4] = {};  // profiling: around lstm_fwd, around lstm_bwd
+    bool small = false;             // B <= 64: fused torso kernels (mlp_*_small_kernel)
+    unsigned* sync = nullptr;       // [0] grid-barrier counter, [1] status (own 64-B allocation)
+    unsigned sync_base = 0;         // counter value at the start of the next fused launch
     bool profiling = false;
     double prof_fwd = 0.0, prof_bwd = 0.0;
     int prof_steps = 0;
@@ -559,6 +839,15 @@ static int forward(fi_farmer* f) {
     else if (R == 2) hipLaunchKernelGGL(lstm_fwd_reg_kernel<2>, grid, blk, 0, s, f->xp, P + o.whh, B, T, f->gates, f->cst, f->hprev, f->cat);
     else hipLaunchKernelGGL(lstm_fwd_reg_kernel<4>, grid, blk, 0, s, f->xp, P + o.whh, B, T, f->gates, f->cst, f->hprev, f->cat);
     if (f->profiling) FI_HIP_CHECK(hipEventRecord(f->pe[1], s));
+    if (f->small) {  // the whole torso + head in one launch
+        SmFwdArgs a{P, f->cat, f->x, {nullptr, f->act[1], f->act[2], f->act[3], f->act[4], f->act[5]}, f->val, B,
+                    SmSync{f->sync, f->sync + 1, f->sync_base}};
+        if (B <= 32) hipLaunchKernelGGL(mlp_fwd_small_kernel<1>, dim3(SM_WG), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL(mlp_fwd_small_kernel<2>, dim3(SM_WG), dim3(256), 0, s, a);
+        f->sync_base += 5u * SM_WG;
+        FI_HIP_CHECK(hipGetLastError());
+        return FI_OK;
+    }
     hipLaunchKernelGGL(cat_x_kernel, dim3((B * XD + 255) / 256), dim3(256), 0, s, f->x, B, f->cat);
     const float* in = f->cat;
     int K = CAT;
@@ -578,6 +867,14 @@ static int backward(fi_farmer* f) {
     const Off& o = f->off;
     float* P = f->params;
     float* Gd = f->grads;
+    if (f->small) {  // criterion, head and the five layers' backward in one launch
+        SmBwdArgs a{P, Gd, f->cat, f->x, {nullptr, f->act[1], f->act[2], f->act[3], f->act[4], f->act[5]}, f->val, f->y,
+                    f->dval, f->loss, {f->dA, f->dB}, f->dcat, B, f->cfg.loss, SmSync{f->sync, f->sync + 1, f->sync_base}};
+        if (B <= 32) hipLaunchKernelGGL(mlp_bwd_small_kernel<1>, dim3(SM_WG), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL(mlp_bwd_small_kernel<2>, dim3(SM_WG), dim3(256), 0, s, a);
+        f->sync_base += 5u * SM_WG;
+        FI_HIP_CHECK(hipGetLastError());
+    } else {
     hipLaunchKernelGGL(loss_kernel, dim3(1), dim3(256), 0, s, f->val, f->y, B, f->cfg.loss, f->dval, f->loss);
     hipLaunchKernelGGL(head_bwd_kernel, dim3(1), dim3(DW), 0, s, f->act[5], P + o.w[6], f->dval, B, Gd + o.w[6],
                        Gd + o.b[6], f->dA);
@@ -593,6 +890,7 @@ static int backward(fi_farmer* f) {
         } else {
             FI_TRY(f32_gemm_nn_dgrad(dcur, B, DW, P + o.w[1], CAT, nullptr, f->dcat, s));
         }
+    }
     }
     {
         const int R = lstm_rows(B);
@@ -687,6 +985,13 @@ extern "C" int fi_farmer_create(const fi_farmer_config* cfg, fi_farmer** out) {
     float* lossf = nullptr;
     A(&lossf, 2);
     f->loss = (double*)lossf;
+    float* syncf = nullptr;
+    A(&syncf, 16);  // its own allocation, zeroed below (Guideline 16: a block of its own)
+    f->sync = (unsigned*)syncf;
+    // the fused torso needs its 128 workgroups co-resident (grid barriers): one per CU at most
+    int cus = 0;
+    if (rc == FI_OK && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, f->dev) != hipSuccess) cus = 0;
+    f->small = f->B <= SM_MAXB && cus >= SM_WG && !std::getenv("FI_FARMER_UNFUSED");
     if (rc == FI_OK && hipStreamCreateWithFlags(&f->stream, hipStreamNonBlocking) != hipSuccess)
         rc = fail(FI_ERR_HIP, "farmer_create: hipStreamCreate failed");
     if (rc == FI_OK && (hipEventCreate(&f->e0) != hipSuccess || hipEventCreate(&f->e1) != hipSuccess))
@@ -700,7 +1005,8 @@ extern "C" int fi_farmer_create(const fi_farmer_config* cfg, fi_farmer** out) {
         if (hipMemsetAsync(f->m, 0, P * 4, s) != hipSuccess || hipMemsetAsync(f->v, 0, P * 4, s) != hipSuccess ||
             hipMemsetAsync(f->params, 0, P * 4, s) != hipSuccess || hipMemsetAsync(f->grads, 0, P * 4, s) != hipSuccess ||
             hipMemsetAsync(f->z, 0, BT * IN * 4, s) != hipSuccess || hipMemsetAsync(f->x, 0, B * XD * 4, s) != hipSuccess ||
-            hipMemsetAsync(f->y, 0, B * 4, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+            hipMemsetAsync(f->y, 0, B * 4, s) != hipSuccess || hipMemsetAsync(f->sync, 0, 64, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
             rc = fail(FI_ERR_HIP, "farmer_create: hipMemsetAsync failed");
     }
     if (rc != FI_OK) {
@@ -774,8 +1080,11 @@ extern "C" int fi_farmer_train_step(fi_farmer* f, const float* z, const float* x
     if (values) FI_HIP_CHECK(hipMemcpyAsync(values, f->val, (size_t)f->B * 4, hipMemcpyDeviceToHost, f->stream));
     if (out) {
         double l = 0.0;
+        unsigned st = 0;
         FI_HIP_CHECK(hipMemcpyAsync(&l, f->loss, sizeof(double), hipMemcpyDeviceToHost, f->stream));
+        if (f->small) FI_HIP_CHECK(hipMemcpyAsync(&st, f->sync + 1, sizeof(st), hipMemcpyDeviceToHost, f->stream));
         FI_HIP_CHECK(hipStreamSynchronize(f->stream));
+        FI_REQUIRE(st == 0, "farmer_train_step: a grid barrier of the fused torso timed out");
         float ms = 0.f;
         FI_HIP_CHECK(hipEventElapsedTime(&ms, f->e0, f->e1));
         out->loss = l;
@@ -792,7 +1101,13 @@ extern "C" int fi_farmer_forward(fi_farmer* f, const float* z, const float* x, i
     FI_HIP_CHECK(hipSetDevice(f->dev));
     FI_TRY(stage_inputs(f, z, x, nullptr, inputs_on_device));
     FI_TRY(forward(f));
-    return d2h(f, f->val, values, (size_t)f->B);
+    FI_TRY(d2h(f, f->val, values, (size_t)f->B));
+    if (f->small) {
+        unsigned st = 0;
+        FI_TRY(d2h(f, (const float*)(f->sync + 1), (float*)&st, 1));
+        FI_REQUIRE(st == 0, "farmer_forward: a grid barrier of the fused torso timed out");
+    }
+    return FI_OK;
 }
 
 extern "C" int fi_farmer_tensor(fi_farmer* f, const char* name, void** ptr, size_t* bytes) {

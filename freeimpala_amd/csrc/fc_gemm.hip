@@ -64,6 +64,21 @@ __device__ __forceinline__ void dma16(fi_i32x4 rsrc, uint32_t voff, uint32_t lds
         : "memory");
 }
 
+// the same with the non-temporal load policy (operands read once: not kept in the caches)
+__device__ __forceinline__ void dma16_nt(fi_i32x4 rsrc, uint32_t voff, uint32_t lds_base) {
+    uint32_t keep;
+    asm volatile(
+        "s_nop 4\n\t"
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %3\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %2, 0 offen nt lds\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(rsrc), "s"(lds_base)
+        : "memory");
+}
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t out_rsrc(void* base, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)bytes, 0x00020000);
 }
@@ -153,7 +168,9 @@ __device__ __forceinline__ int nt_chunk(int c, int row) {
 
 // ---------------------------------------------------------------- NT kernel
 // OPT bits: 1 = s_setprio 1 around each MFMA cluster, 2 = nontemporal (streaming) output stores,
-// 4 = accumulators in AGPRs (for 4-wave tiles of 128 x 128 per wave)
+// 4 = accumulators in AGPRs (for 4-wave tiles of 128 x 128 per wave), 8 = non-temporal loads of
+// the Y operand (the frame rows), 16 = the next step's DMA issued after the first sub-step's
+// fragment reads (their LDS latency overlaps the issue), 32 = ... after the first sub-step's MFMAs
 template <int BX, int BY, int WX, int WY, int BK, int NS, class Epi, int OPT = 0>
 __global__ __launch_bounds__(64 * WX * WY) void fc_nt_kernel(const __bf16* __restrict__ X, const __bf16* __restrict__ Y,
                                                     int NY, int K, int ntx, int ntiles, Epi epi) {
@@ -193,7 +210,12 @@ __global__ __launch_bounds__(64 * WX * WY) void fc_nt_kernel(const __bf16* __res
             const bool isx = pi < PX;
             const int prow = (isx ? pi : pi - PX) * RPP + lane / (BK / 8);
             const int ch = nt_chunk<BK>(lane % (BK / 8), prow);
-            dma16(isx ? rx : ry, (uint32_t)((prow * K + is_kt * BK + ch * 8) * 2), sb + (uint32_t)pi * 1024u);
+            if constexpr (OPT & 8) {
+                if (isx) dma16(rx, (uint32_t)((prow * K + is_kt * BK + ch * 8) * 2), sb + (uint32_t)pi * 1024u);
+                else dma16_nt(ry, (uint32_t)((prow * K + is_kt * BK + ch * 8) * 2), sb + (uint32_t)pi * 1024u);
+            } else {
+                dma16(isx ? rx : ry, (uint32_t)((prow * K + is_kt * BK + ch * 8) * 2), sb + (uint32_t)pi * 1024u);
+            }
         }
         if (++is_kt == nk) is_kt = 0, ++is_tile;
     };
@@ -216,7 +238,9 @@ __global__ __launch_bounds__(64 * WX * WY) void fc_nt_kernel(const __bf16* __res
             const int ahead = min(D - 1, total - 1 - it);
             vm_wait_rt(ahead * PW + (it - last_epi <= D ? NST : 0));
             lds_barrier();
-            if (it + D < total) issue(it + D);
+            if constexpr (!(OPT & 48)) {
+                if (it + D < total) issue(it + D);
+            }
             const char* sx = lds + (it % NS) * SLOT;
             const char* sy = sx + BX * BK * 2;
 #pragma unroll
@@ -233,6 +257,9 @@ __global__ __launch_bounds__(64 * WX * WY) void fc_nt_kernel(const __bf16* __res
                     const int row = wy * TY + g * 16 + (lane & 15);
                     fb[g] = *(const bf16x8*)(sy + row * (BK * 2) + (nt_chunk<BK>(ch, row) << 4));
                 }
+                if constexpr ((OPT & 16) != 0) {
+                    if (s == 0 && it + D < total) issue(it + D);
+                }
                 if constexpr (OPT & 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
                 for (int f = 0; f < FX; ++f)
@@ -240,6 +267,9 @@ __global__ __launch_bounds__(64 * WX * WY) void fc_nt_kernel(const __bf16* __res
                     for (int g = 0; g < FY; ++g)
                         acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[f], fb[g], acc[f][g], 0, 0, 0);
                 if constexpr (OPT & 1) __builtin_amdgcn_s_setprio(0);
+                if constexpr ((OPT & 32) != 0) {
+                    if (s == 0 && it + D < total) issue(it + D);
+                }
             }
         }
         const int t = lg + tile_it * NG;

@@ -508,7 +508,8 @@ __global__ __launch_bounds__(64 * VtLayout<A>::NW, VtLayout<A>::WPS) void vtrace
 }
 
 // ------------------------------------------------------------------------------------
-// Kernel 3 (vtrace_seq_kernel<A>, the default for T <= 128): a persistent 256-thread
+// Kernel 3 (vtrace_seq_kernel<A>, on request only -- measured slower than kernel 1, DESIGN.md
+// section 5): a persistent 256-thread
 // workgroup walks column PAIRS p = lg, lg + G, ... and owns each pair for the WHOLE sequence,
 // so the only serial dependency of V-trace (the scalar carry acc_{t+1}) is resolved by one
 // in-register scan plus one cross-wave combine per pair -- no chain of time chunks.
@@ -822,14 +823,12 @@ static void launch_seq(const VtArgs& a, int nblk, hipStream_t s) {
     hipLaunchKernelGGL(vtrace_seq_kernel<A>, dim3(nblk), dim3(VtSeq<A>::NT), VtSeq<A>::lds_bytes(a.T), s, a);
 }
 // persistent grid of the sequence kernel: two workgroups per CU (LDS: two pair slots each)
+// (the CU count is read from the calling thread's current device each time: handles on
+// different devices launch from their own threads, so no cached process-wide value)
 static int seq_grid(int B) {
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
-        hipDeviceProp_t prop;
-        cus = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
-                  ? prop.multiProcessorCount : 256;
-    }
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess)
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     return std::max(1, std::min(B / 2, 2 * cus));
 }
 

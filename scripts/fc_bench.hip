@@ -78,12 +78,18 @@ int main(int argc, char** argv) {
 #define WGV(nm, S, ...) add("wgrd " nm, 2, [&](hipStream_t st, int k) { return fc_wgrad_impl<__VA_ARGS__>(a3, dh, slab, dw[k], R, st, S); }, dw[0], dw[1], (size_t)FCK * FCO * 4)
     // the shipped configurations first (fc_gemm.hip FC_*_CFG), then alternatives
     FWDV("256x256 w4x2 bk64 ns2 prio", 256, 256, 4, 2, 64, 2, 1);
+    FWDV("256x256 w4x2 bk64 ns2 prio ntY", 256, 256, 4, 2, 64, 2, 1 | 8);
+    FWDV("256x256 w4x2 bk64 ns2 prio iss@frag", 256, 256, 4, 2, 64, 2, 1 | 16);
+    FWDV("256x256 w4x2 bk64 ns2 prio iss@mid", 256, 256, 4, 2, 64, 2, 1 | 32);
+    FWDV("256x256 w4x2 bk32 ns3 prio", 256, 256, 4, 2, 32, 3, 1);
+    FWDV("256x256 w4x2 bk32 ns4 prio", 256, 256, 4, 2, 32, 4, 1);
+    FWDV("256x256 w4x2 bk32 ns4 prio ntY", 256, 256, 4, 2, 32, 4, 1 | 8);
     DGV("224x256 w1x8 bk64 ns2 prio", 224, 256, 1, 8, 64, 2, 1);
-    DGV("224x256 w2x4 bk64 ns2 prio", 224, 256, 2, 4, 64, 2, 1);
-    DGV("224x256 w2x4 bk64 ns2", 224, 256, 2, 4, 64, 2, 0);
-    DGV("224x256 w2x4 bk32 ns4 prio", 224, 256, 2, 4, 32, 4, 1);
-    DGV("448x128 w4x2 bk64 ns2 prio", 448, 128, 4, 2, 64, 2, 1);
-    DGV("224x128 w2x4 bk64 ns2 prio", 224, 128, 2, 4, 64, 2, 1);
+    DGV("224x256 w1x8 bk64 ns2 prio iss@frag", 224, 256, 1, 8, 64, 2, 1 | 16);
+    DGV("224x256 w1x8 bk64 ns2 prio iss@mid", 224, 256, 1, 8, 64, 2, 1 | 32);
+    DGV("224x256 w1x8 bk32 ns3 prio", 224, 256, 1, 8, 32, 3, 1);
+    DGV("224x256 w1x8 bk32 ns4 prio", 224, 256, 1, 8, 32, 4, 1);
+    DGV("224x256 w1x8 bk64 ns2 prio ntst", 224, 256, 1, 8, 64, 2, 1 | 2);
     WGV("256x224 w4x2 bk64 ns2", 9, 256, 224, 4, 2, 64, 2);
     // hipBLASLt (the default fwd / dgrad today), own output buffers: not bit-comparable
     __bf16 *hb, *db;

@@ -9,7 +9,7 @@ mkdir -p "$OUT"
 TAG=$1
 shift
 TARGETS=${*:-tests}
-timeout -k 10 ${TEST_TIMEOUT:-600} python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu $TARGETS \
+timeout -k 10 ${TEST_TIMEOUT:-600} python -u -m pytest -x -v ${PYTEST_ARGS:-} --timeout 120 --timeout-method thread -m gpu $TARGETS \
     > "$OUT/pytest_$TAG.log" 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -4 "$OUT/pytest_$TAG.log"
 [ $rc -ne 0 ] && { grep -E "FAILED|Error|assert" "$OUT/pytest_$TAG.log" | head -20; exit $rc; }

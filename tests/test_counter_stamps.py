@@ -16,7 +16,7 @@ def test_source_hash_covers_the_learner_sources_only():
     assert "freeimpala_amd/csrc/farmer.hip" not in files
     h = build_info.source_hash()
     assert len(h) == 16 and h == build_info.source_hash()
-    assert build_info.stamp({"arch": "x"}) == {"source_hash": h, "arch": "x"}
+    assert build_info.stamp({"arch": "x"}) == {"source_hash": h, "runtime": build_info.runtime_key(), "arch": "x"}
 
 
 def _fake_root(tmp_path, stamp):
@@ -24,7 +24,8 @@ def _fake_root(tmp_path, stamp):
     (tmp_path / "profiles").mkdir()
     for kind, body in (("traffic", {"conv21_bwd": {"hbm_bytes_per_launch": 123}}),
                        ("mfma", {"conv21_bwd": {"mfma_util": 0.5}})):
-        d = dict(body, _build={"source_hash": stamp})
+        from freeimpala_amd import build_info
+        d = dict(body, _build={"source_hash": stamp, "runtime": build_info.runtime_key()})
         (tmp_path / "profiles" / f"zz_pmc_{kind}_atari.json").write_text(json.dumps(d))
     return str(tmp_path)
 
@@ -51,3 +52,16 @@ def test_bench_refuses_counters_of_another_shape(tmp_path, monkeypatch):
     monkeypatch.setattr(bench, "ROOT", _fake_root(tmp_path, build_info.source_hash()))
     tr, mf, info = bench.load_counters("atari", (100, 512, 18))
     assert tr == {} and mf == {} and "T=100 B=4096" in info["note"]
+
+
+def test_bench_refuses_counters_taken_under_other_switches(tmp_path, monkeypatch):
+    """the same sources run different kernels under FI_* switches (e.g. FI_FC_OWN,
+    FI_BWD_UNFUSED): a pass stamped under one setting is not attached to a line timed under
+    another."""
+    import bench
+    from freeimpala_amd import build_info
+    monkeypatch.delenv("FI_BWD_UNFUSED", raising=False)
+    monkeypatch.setattr(bench, "ROOT", _fake_root(tmp_path, build_info.source_hash()))
+    monkeypatch.setenv("FI_BWD_UNFUSED", "1")
+    tr, mf, info = bench.load_counters("atari", (100, 4096, 18))
+    assert tr == {} and mf == {} and info["runtime"]["env"] == {"FI_BWD_UNFUSED": "1"}

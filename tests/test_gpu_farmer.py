@@ -147,3 +147,34 @@ def test_farmer_reference_interface_and_loss_decreases():
     with pytest.raises(ValueError):
         farmer.run_single_training_iteration(M, z, x, t, farmer.get_loss_function("mae"), opt, None)
     M.close()
+
+
+@pytest.mark.parametrize("B,T,loss", [(32, 10, "mse"), (7, 4, "huber"), (64, 5, "mae"), (33, 3, "mse")])
+def test_fused_small_batch_torso_matches_layer_kernels(B, T, loss, monkeypatch):
+    """B <= 64 runs the torso + head as one grid-synchronised launch per direction
+    (mlp_fwd_small / mlp_bwd_small, 128 workgroups, five grid barriers each); FI_FARMER_UNFUSED
+    forces the per-layer GEMM path. Same step on both: values and loss 1e-5, every gradient
+    tensor within 1e-5 relative L2 (different fp32 summation order), and the fused step
+    repeats bit for bit (fixed-order partial sums, no atomics on data)."""
+    from oracle import farmer_oracle as fo
+    p0 = fo.gen_params(21)
+    z, x, y = fo.gen_inputs(22, B, T)
+    out = {}
+    for mode in ("unfused", "fused", "fused2"):
+        if mode == "unfused":
+            monkeypatch.setenv("FI_FARMER_UNFUSED", "1")
+        else:
+            monkeypatch.delenv("FI_FARMER_UNFUSED", raising=False)
+        M = _model(B, T, loss, "sgd", 1e-2, p0)
+        lv, val = M.train_step(z, x, y, with_values=True)
+        out[mode] = (lv, val, M.get_grads(), M.get_params())
+        M.close()
+    (lu, vu, gu, _), (lf, vf, gf, pf), (l2, v2, g2, p2) = out["unfused"], out["fused"], out["fused2"]
+    np.testing.assert_allclose(vf, vu, rtol=1e-5, atol=1e-6)
+    assert abs(lf - lu) <= 1e-5 * max(1.0, abs(lu))
+    for n, (a, b, s) in fo.offsets().items():
+        _grad_close(gf[a:b], gu[a:b], n)
+    assert lf == l2
+    np.testing.assert_array_equal(vf, v2)
+    np.testing.assert_array_equal(gf, g2)
+    np.testing.assert_array_equal(pf, p2)

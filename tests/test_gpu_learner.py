@@ -446,6 +446,72 @@ def test_two_device_data_parallel_matches_full_batch_and_oracle(orc):
         r.close()
 
 
+def test_two_device_atari_bucketed_overlap_matches_full_batch():
+    """The Atari network on two devices: the three gradient buckets (fc + heads, conv3,
+    conv1 + conv2) are all-reduced on the comm stream while the conv backward still runs, so
+    the overlapped path gets a real peer. Each replica synthesises its half of the global batch
+    (columns indexed globally), both end bit-identical, and equal to one device stepping the
+    whole batch up to the order of the fp32 gradient sums (per-frame activations are
+    grid-independent, the slab reductions are not). Skipped on one-GPU boxes."""
+    from concurrent.futures import ThreadPoolExecutor
+    from freeimpala_amd.learner import DeviceLearner
+    _two_devices()
+    T, B = 2, 32
+    full = mk(arch="atari", T=T, B=B, seed=6)
+    reps = [mk(arch="atari", T=T, B=B // 2, seed=6, device=d) for d in (0, 1)]
+    DeviceLearner.comm_init_all(reps)
+    full.synth(seed=12, b_global=B, b_offset=0)
+    for i, r in enumerate(reps):
+        r.synth(seed=12, b_global=B, b_offset=i * B // 2)
+    p0 = full.get_params()
+    for r in reps:
+        np.testing.assert_array_equal(r.get_params(), p0)
+    for _ in range(2):
+        st = full.step_resident()
+        with ThreadPoolExecutor(2) as ex:
+            res = list(ex.map(lambda i: reps[i].step_resident(), (0, 1)))
+        assert abs(res[0]["total_loss"] + res[1]["total_loss"] - st["total_loss"]) <= 1e-5 * max(1, abs(st["total_loss"]))
+    assert [r.comm_info()["buckets_last_step"] for r in reps] == [3, 3]
+    np.testing.assert_array_equal(reps[0].get_params(), reps[1].get_params())
+    scaled_close(reps[0].get_params(), full.get_params(), 1e-6, "2-device vs 1-device Atari params")
+    for r in reps + [full]:
+        r.close()
+
+
+@pytest.mark.parametrize("nproc", [1, 2])
+@pytest.mark.parametrize("arch", ["mlp", "atari"])
+def test_two_process_attach_comm_matches_single_device(arch, nproc, tmp_path):
+    """bench.py's N > 1 form: processes under torch.distributed.run, one device each, the
+    RCCL unique id broadcast over gloo, fi_learner_attach_comm, SGD steps with the in-step
+    all-reduce (tests/dist_attach_worker.py). Replicas bit-identical; equal to one device
+    stepping the whole batch (1e-6 scaled); the shard losses sum to the full batch's.
+    nproc=2 is skipped on one-GPU boxes; nproc=1 runs the same script on one GPU with a
+    one-rank communicator (FI_COMM_SINGLE), so the launcher path is exercised everywhere."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+    if nproc == 2:
+        _two_devices()
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(root, "tests", "dist_attach_worker.py"), "--arch", arch, "--out", str(tmp_path)]
+    env = dict(os.environ, FI_COMM_SINGLE="1") if nproc == 1 else None
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=root, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = json.loads((tmp_path / "result.json").read_text())
+    assert res["world"] == nproc and res["comm"]["nranks"] == nproc and res["buckets_last_step"] == 3
+    assert res["replicas_identical"]
+    assert res["max_scaled_diff_vs_one_device"] <= 1e-6, res
+    for a, b in zip(res["loss_sum"], res["one_device_loss"]):
+        assert abs(a - b) <= 1e-5 * max(1.0, abs(b)), res
+
+
 def test_two_device_reject_is_agreed(orc):
     """A bad action in ONE replica's shard: the all-reduced reject flag makes BOTH replicas
     skip the optimizer (both raise FI_ERR_INVALID, parameters and version unchanged on both), so

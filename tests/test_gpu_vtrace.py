@@ -112,7 +112,7 @@ def test_vtrace_adversarial_clipping(orc):
 def test_vtrace_full_size_T100_B4096(orc, variant):
     """BASELINE config size (T=100, B=4096, A=18): full elementwise parity with the oracle
     plus the size-independent property sum(pg_adv-weighted) via the loss scalars; the chunked
-    kernel (1) and the whole-sequence kernel (3, the default at T <= 128)."""
+    kernel (1, the default) and the whole-sequence kernel (3, on request only)."""
     case = rand_case(4096, 100, 4096, 18)
     ref = orc.vtrace_loss(*case)
     out = run_vtrace(*case, variant=variant)
