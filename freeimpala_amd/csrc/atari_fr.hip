@@ -33,86 +33,7 @@ typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
-#ifdef FI_STAMPS  // timing experiment: wave-0 s_memrealtime stamps per workgroup, printed by the launcher
-__device__ unsigned long long fi_stamps[256 * 32];
-#define ST_DECL unsigned long long st_[32]; int sn_ = 0;
-#define ST() do { if (sn_ < 32) st_[sn_++] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#define ST_FLUSH() do { if (threadIdx.x == 0 && blockIdx.x < 256) for (int i_ = 0; i_ < 32; ++i_) fi_stamps[blockIdx.x * 32 + i_] = i_ < sn_ ? st_[i_] : 0ull; } while (0)
-#include <cstdio>
-#include <vector>
-#include <algorithm>
-static void st_report(const char* name) {
-    static const char* names[8];
-    static int calls[8];
-    int k = 0;
-    while (k < 8 && names[k] && names[k] != name) ++k;
-    if (k == 8) return;
-    names[k] = name;
-    if (++calls[k] != 4) return;
-    (void)hipDeviceSynchronize();
-    std::vector<unsigned long long> h(256 * 32);
-    (void)hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(fi_stamps), h.size() * 8);
-    unsigned long long t0 = ~0ull;
-    for (int b = 0; b < 256; ++b) t0 = std::min(t0, h[b * 32]);
-    std::fprintf(stderr, "[stamps %s] us rel. to first start: idx: min/med/max\n", name);
-    for (int i = 0; i < 32; ++i) {
-        std::vector<double> v;
-        for (int b = 0; b < 256; ++b) if (h[b * 32 + i]) v.push_back((h[b * 32 + i] - t0) * 0.01);
-        if (v.empty()) break;
-        std::sort(v.begin(), v.end());
-        std::fprintf(stderr, "  %2d: %8.2f %8.2f %8.2f\n", i, v.front(), v[v.size() / 2], v.back());
-    }
-}
-#else
-#define ST_DECL
-#define ST() do {} while (0)
-#define ST_FLUSH() do {} while (0)
-static void st_report(const char*) {}
-#endif
 
-#ifdef FI_PHASES  // timing experiment: per-phase clock sums of waves 0 and 4, per workgroup
-__device__ unsigned long long fi_phases[1024 * 16];
-#define PH_DECL unsigned long long ph_[6] = {0, 0, 0, 0, 0, 0}, pt_ = __builtin_amdgcn_s_memtime(), rt0_ = __builtin_amdgcn_s_memrealtime(), ct0_ = pt_; int pn_ = 0;
-#define PH(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); ph_[k] += t_ - pt_; pt_ = t_; } while (0)
-#define PH_ITER() (++pn_)
-#define PH_FLUSH() do { const int w_ = wave_id(); if ((threadIdx.x & 63) == 0 && (w_ == 0 || w_ == 4) && blockIdx.x < 1024) { \
-    for (int k_ = 0; k_ < 6; ++k_) fi_phases[blockIdx.x * 16 + (w_ ? 8 : 0) + k_] = ph_[k_]; \
-    fi_phases[blockIdx.x * 16 + (w_ ? 8 : 0) + 7] = pn_; \
-    fi_phases[blockIdx.x * 16 + (w_ ? 8 : 0) + 6] = ((__builtin_amdgcn_s_memtime() - ct0_) << 20) / max(1ull, __builtin_amdgcn_s_memrealtime() - rt0_); } } while (0)
-#include <cstdio>
-#include <vector>
-static void ph_report(const char* name, int grid) {
-    static const char* names[8];
-    static int calls[8];
-    int k = 0;
-    while (k < 8 && names[k] && names[k] != name) ++k;
-    if (k == 8) return;
-    names[k] = name;
-    if (++calls[k] != 4) return;
-    (void)hipDeviceSynchronize();
-    std::vector<unsigned long long> h(1024 * 16);
-    (void)hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(fi_phases), h.size() * 8);
-    for (int r = 0; r < 2; ++r) {
-        double sum[6] = {0}, n = 0;
-        for (int b = 0; b < grid && b < 1024; ++b) {
-            for (int k = 0; k < 6; ++k) sum[k] += (double)h[b * 16 + 8 * r + k];
-            n += (double)h[b * 16 + 8 * r + 7];
-        }
-        double mhz = 0;  // shader clocks per 100 MHz real-time tick (s_memrealtime), mean over workgroups
-        int nb = 0;
-        for (int b = 0; b < grid && b < 1024; ++b, ++nb) mhz += (double)h[b * 16 + 8 * r + 6] / (1 << 20) * 100.0;
-        std::fprintf(stderr, "[phases %s wave %d] clk/frame:", name, 4 * r);
-        for (int k = 0; k < 6; ++k) std::fprintf(stderr, " %.0f", sum[k] / (n > 0 ? n : 1));
-        std::fprintf(stderr, "  clock %.0f MHz\n", nb ? mhz / nb : 0.0);
-    }
-}
-#else
-#define PH_DECL
-#define PH(k) do {} while (0)
-#define PH_ITER() do {} while (0)
-#define PH_FLUSH() do {} while (0)
-static void ph_report(const char*, int) {}
-#endif
 
 namespace c1 {
 constexpr int FRAME_LOADS = 84 * 84 * 4 / 16;       // 1764 16-byte loads per frame
@@ -224,23 +145,16 @@ __global__ __launch_bounds__(512, 2) void conv1_fwd_fr(const uint8_t* __restrict
     const int nst = w == 0 ? 4 : 3;  // a1 stores per frame (one per tile)
 
     const int nmine = nframes > (int)blockIdx.x ? (nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
-    ST_DECL
-    ST();
     int issued = 0, m0 = 0, m1 = 0;
     if (nmine > 0) issued += c1_issue_raw(frames + (size_t)blockIdx.x * 28224, lds0, w, lane);
     m0 = issued;
     if (nmine > 1) issued += c1_issue_raw(frames + (size_t)(blockIdx.x + gridDim.x) * 28224, lds0 + c1::RAW, w, lane);
     m1 = issued;
-    PH_DECL
     for (int it = 0; it < nmine; ++it) {
         const int f = blockIdx.x + it * gridDim.x;
         const char* raw = smem + (it & 1) * c1::RAW;
-        PH(5);
         wait_vmcnt(issued - m0);
-        PH(0);
         lds_barrier();  // raw frame landed; every wave done with the previous image
-        PH(1);
-        if (it < 6) ST();
 #pragma unroll
         for (int i = 0; i < (c1::FRAME_LOADS + 511) / 512; ++i) {
             const int u = threadIdx.x + 512 * i;
@@ -251,16 +165,12 @@ __global__ __launch_bounds__(512, 2) void conv1_fwd_fr(const uint8_t* __restrict
                 *(bf16x8*)(img + c1::PLANE + 16 * u) = hi;
             }
         }
-        PH(2);
         lds_barrier();  // image ready; raw slot free
-        PH(1);
-        if (it < 6) ST();
         int m2 = issued;
         if (it + 2 < nmine) {
             issued += c1_issue_raw(frames + (size_t)(f + 2 * gridDim.x) * 28224, lds0 + (it & 1) * c1::RAW, w, lane);
             m2 = issued;
         }
-        PH(4);
         u32x4* dst = (u32x4*)(a1 + (size_t)f * 12800);
         // B fragments of tile t: pixel pair (4ox + 2g..+1) of input row 4oy + ks -> plane g&1,
         // unit (4oy + ks) * 21 + ox + (g>>1)
@@ -307,15 +217,10 @@ __global__ __launch_bounds__(512, 2) void conv1_fwd_fr(const uint8_t* __restrict
         }
         if (w == 0) store(24, tile(fb[1]));
         issued += nst;
-        PH(3);
-        PH_ITER();
         m0 = m1;
         m1 = m2;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    ST();
-    ST_FLUSH();
-    PH_FLUSH();
 }
 
 // ---------------------------------------------------------------------------------
@@ -397,14 +302,10 @@ __global__ __launch_bounds__(512, 2) void conv1_wgrad_fr(const uint8_t* __restri
     int issued = 0, mk_raw = 0, mk_dy0 = 0, mk_dy1 = 0;
     if (nmine > 0) { issued += issue_raw(0); mk_raw = issued; issued += issue_dy(0); mk_dy0 = issued; }
     if (nmine > 1) { issued += issue_dy(1); mk_dy1 = issued; }
-    PH_DECL
     for (int it = 0; it < nmine; ++it) {
         const char* dy = smem + c1::RAW + (it % 3) * c1::OUT;
-        PH(5);
         wait_vmcnt(issued - max(mk_raw, mk_dy0));
-        PH(0);
         lds_barrier();  // raw frame + da1 tile landed; previous frame consumed by every wave
-        PH(1);
         int mk_dy2 = 0;
         if (it + 2 < nmine) { issued += issue_dy(it + 2); mk_dy2 = issued; }
 #pragma unroll
@@ -417,11 +318,8 @@ __global__ __launch_bounds__(512, 2) void conv1_wgrad_fr(const uint8_t* __restri
                 *(bf16x8*)(img + c1::PLANE + 16 * u) = hi;
             }
         }
-        PH(2);
         lds_barrier();  // image ready; raw slot free
-        PH(1);
         if (it + 1 < nmine) { issued += issue_raw(it + 1); mk_raw = issued; }
-        PH(4);
         const char* DB = dy + wb0;
         auto load = [&](int j, bf16x8* d) {  // [0] da1, [1..4] A of k-tiles kt = 0..3
             d[0] = tr2(DB + 4096 * j, DB + 256 + 4096 * j);
@@ -455,13 +353,10 @@ __global__ __launch_bounds__(512, 2) void conv1_wgrad_fr(const uint8_t* __restri
             }
         }
         if (mg == 0) step(fb[0]);
-        PH(3);
-        PH_ITER();
         mk_dy0 = mk_dy1;
         mk_dy1 = mk_dy2;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    PH_FLUSH();
     // reduce the four m-groups in LDS (fixed order mg = 0..3), one k-group per round:
     // red[mg][kt][r][lane] -> slab rows k = 32(4kg + kt) + (r&3) + 8(r>>2) + 4(lane>>5), col lane&31
     float* red = (float*)smem;
@@ -500,8 +395,6 @@ int conv1_fwd_fr_launch(const uint8_t* frames, const __bf16* w1t, const float* b
                         int nframes, int grid, hipStream_t s) {
     hipLaunchKernelGGL(conv1_fwd_fr, dim3(grid), dim3(512), 0, s, frames, w1t, bias, a1, nframes);
     FI_HIP_CHECK(hipGetLastError());
-    st_report("conv1_fwd");
-    ph_report("conv1_fwd", grid);
     return FI_OK;
 }
 
@@ -509,7 +402,6 @@ int conv1_wgrad_fr_launch(const uint8_t* frames, const __bf16* da1, float* slab,
                           int nframes, int grid, hipStream_t s) {
     hipLaunchKernelGGL(conv1_wgrad_fr, dim3(grid), dim3(512), 0, s, frames, da1, slab, cs_slab, nframes);
     FI_HIP_CHECK(hipGetLastError());
-    ph_report("conv1_wgrad", grid);
     return FI_OK;
 }
 
@@ -689,15 +581,9 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
         }
     };
     constexpr int NSTEP = TPW * G::KS;  // (tile, k-step) steps per iteration
-    ST_DECL
-    ST();
-    PH_DECL
     for (int it = 0; it < niter; ++it) {
         const char* X = smem + (it & 1) * FPI * G::XB;
-        PH(5);
         lds_barrier();  // iteration it's image written; iteration it-1 consumed by every wave
-        PH(1);
-        if (it < 5) ST();
         // tile-outer steps: each tile's 2*KS MFMAs end in its 16-byte store; B fragments are
         // read PD steps ahead of their MFMAs
         constexpr int PD = 4;
@@ -737,13 +623,10 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
                 acc1 = f32x4{};
             }
         }
-        PH(3);
         if (it + 1 < niter) {
             wait_vmcnt(issued - mk[0]);  // own pieces of iteration it + 1 landed (stores may fly)
-            PH(0);
             reshuffle(it + 1);           // image slot (it+1)&1 was last read in iteration it-1
         }
-        PH(2);
         int mnew = issued;
         if (it + 1 + STG < niter) {
             issued += issue(it + 1 + STG);  // into the staging buffer just emptied
@@ -752,21 +635,14 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
 #pragma unroll
         for (int q = 0; q + 1 < STG; ++q) mk[q] = mk[q + 1];
         mk[STG - 1] = mnew;
-        PH(4);
-        PH_ITER();
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    ST();
-    ST_FLUSH();
-    PH_FLUSH();
 }
 
 int conv2_fwd_fr_launch(const __bf16* a1, const __bf16* w2t, const float* bias, __bf16* a2, int nframes,
                         int grid, hipStream_t s) {
     hipLaunchKernelGGL(conv_fwd_fr<2>, dim3(grid), dim3(512), 0, s, a1, w2t, bias, a2, nframes);
     FI_HIP_CHECK(hipGetLastError());
-    st_report("conv2_fwd");
-    ph_report("conv2_fwd", grid);
     return FI_OK;
 }
 
@@ -774,8 +650,6 @@ int conv3_fwd_fr_launch(const __bf16* a2, const __bf16* w3t, const float* bias, 
                         int grid, hipStream_t s) {
     hipLaunchKernelGGL(conv_fwd_fr<3>, dim3(grid), dim3(512), 0, s, a2, w3t, bias, a3, nframes);
     FI_HIP_CHECK(hipGetLastError());
-    st_report("conv3_fwd");
-    ph_report("conv3_fwd", grid);
     return FI_OK;
 }
 
@@ -844,21 +718,16 @@ __global__ __launch_bounds__(512, 2) void conv12_fwd_fr(const uint8_t* __restric
         const float inv255 = 1.0f / 255.0f;
         const int ntile = w == 0 ? 7 : 6;  // tiles w + 4tt < 25
         u32x4 held[7];                     // a1 of the previous frame, tile tt
-        PH_DECL
         for (int it = 0; it <= nmine; ++it) {
             const int f = blockIdx.x + it * gridDim.x;
-            PH(5);
             lds_barrier();  // B1: raw(it) landed (waited by its issuers); conv1 image and a1 image free
-            PH(1);
             if (it >= 1) {  // a1(it-1) -> conv2 image (pixel q, chunk g)
 #pragma unroll
                 for (int tt = 0; tt < 7; ++tt)
                     if (tt < ntile) *(u32x4*)(x2 + 16 * f2_dst(4 * ((w + 4 * tt) * 16 + si) + g)) = held[tt];
             }
             if (it < nmine) c12_convert(smem + (it & 1) * c1::RAW, img, tid);
-            PH(2);
             lds_barrier();  // B2: conv1 image and conv2 image complete
-            PH(1);
             if (it < nmine) {
                 u32x4* dst = (u32x4*)(a1 + (size_t)f * 12800);
                 auto load = [&](int t, bf16x8* d) {
@@ -904,11 +773,8 @@ __global__ __launch_bounds__(512, 2) void conv12_fwd_fr(const uint8_t* __restric
                     }
                 }
             }
-            PH(3);
-            PH_ITER();
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        PH_FLUSH();
     } else {
         // ---------------- conv2 role (+ raw-frame DMA)
         const int wr = w - 4, chh = wr & 1, pg = wr >> 1;
@@ -946,23 +812,16 @@ __global__ __launch_bounds__(512, 2) void conv12_fwd_fr(const uint8_t* __restric
         m0 = issued;
         if (nmine > 1) issued += issue_raw(1, 1);
         m1 = issued;
-        PH_DECL
         for (int it = 0; it <= nmine; ++it) {
-            PH(5);
             if (it < nmine) wait_vmcnt(issued - m0);  // own pieces of raw(it) landed
-            PH(0);
             lds_barrier();  // B1
-            PH(1);
             if (it < nmine) c12_convert(smem + (it & 1) * c1::RAW, img, tid);
-            PH(2);
             lds_barrier();  // B2: raw slot it&1 converted; a1(it-1) in the conv2 image
-            PH(1);
             int m2 = issued;
             if (it + 2 < nmine) {
                 issued += issue_raw(it + 2, it & 1);
                 m2 = issued;
             }
-            PH(4);
             if (it >= 1) {  // conv2 of frame it-1 from the a1 image
                 const int k = it - 1;
                 u32x4* dst = (u32x4*)(a2 + (size_t)(blockIdx.x + k * gridDim.x) * 5184);
@@ -999,13 +858,10 @@ __global__ __launch_bounds__(512, 2) void conv12_fwd_fr(const uint8_t* __restric
                 }
                 issued += 3;  // every tile has valid pixels: three store instructions
             }
-            PH(3);
-            PH_ITER();
             m0 = m1;
             m1 = m2;
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        PH_FLUSH();
     }
 }
 
@@ -1015,7 +871,6 @@ int conv12_fwd_fr_launch(const uint8_t* frames, const __bf16* w1t, const float* 
     hipLaunchKernelGGL(conv12_fwd_fr, dim3(grid), dim3(512), 0, s, frames, w1t, b1, w2t, b2, a1, a2, nframes,
                        a1_planar);
     FI_HIP_CHECK(hipGetLastError());
-    ph_report("conv12_fwd", grid);
     return FI_OK;
 }
 
@@ -1116,42 +971,28 @@ __device__ __forceinline__ void c2_frames(const C2Ctx& c, char* smem, int nst, W
     __syncthreads();
     const int npw = w == 0 ? 11 : (w < 4 ? 10 : 0);  // pieces per wave
     const int nmine = c.nframes > (int)blockIdx.x ? (c.nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
-    ST_DECL
-    ST();
     int issued = 0, m0 = 0, m1 = 0;
     for (int i = 0; i < 2 && i < nmine; ++i) {
         if (w < 4) c2_issue(c, tab, blockIdx.x + i * gridDim.x, lds0 + i * c2::SLOT, w, lane);
         issued += npw;
         if (i == 0) m0 = issued; else m1 = issued;
     }
-    PH_DECL
     for (int it = 0; it < nmine; ++it) {
         const int f = blockIdx.x + it * gridDim.x;
-        PH(5);
         wait_vmcnt(issued - m0);
-        PH(0);
         lds_barrier();  // frame it landed; frame it-1 consumed by every wave
-        PH(1);
-        if (it < 5) ST();
         int m2 = 0;
         if (it + 2 < nmine) {
             if (w < 4) c2_issue(c, tab, f + 2 * gridDim.x, lds0 + ((it + 2) % 3) * c2::SLOT, w, lane);
             issued += npw;
             m2 = issued;
         }
-        PH(2);
         work(smem + (it % 3) * c2::SLOT, f);
-        PH(3);
-        PH_ITER();
         issued += nst;
-        if (it < 5) ST();
         m0 = m1;
         m1 = m2;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    ST();
-    ST_FLUSH();
-    PH_FLUSH();
 }
 
 __global__ __launch_bounds__(512, 2) void conv2_bwd_fr(const __bf16* __restrict__ a1,
@@ -1320,8 +1161,6 @@ int conv2_bwd_fr_launch(const __bf16* a1, const __bf16* da2, const __bf16* w2d, 
     hipLaunchKernelGGL(conv2_bwd_fr, dim3(grid), dim3(512), 0, s, a1, da2, w2d, da1,
                        slab, cs_slab, nframes);
     FI_HIP_CHECK(hipGetLastError());
-    st_report("conv2_bwd");
-    ph_report("conv2_bwd", grid);
     return FI_OK;
 }
 
@@ -1516,13 +1355,9 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
             load_raw(0);
             issued += c21::NRAW_A;
         }
-        PH_DECL
         for (int it = 0; it < nmine; ++it) {
-            PH(5);
             wait_vmcnt(issued - m_dy);  // own pieces of da2(it) landed (a1(it) is older)
-            PH(0);
             lds_barrier();  // B1: frame it's images in LDS; frame it-1's D and image consumed
-            PH(1);
             {
                 const char* XA = smem + c21::O_AX + (it & 1) * c21::AXB + ba0;
                 const char* XB_ = DY + bb0;
@@ -1562,7 +1397,6 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                     }
                 }
             }
-            PH(2);
 #pragma unroll
             for (int i = 0; i < c21::NRAW_A; ++i) {  // raw(it) -> bf16 pair-plane image (free since B1)
                 const int u = tid + 256 * i;
@@ -1580,19 +1414,14 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                 load_raw(it + 1);
                 issued += c21::NRAW_A;
             }
-            PH(3);
             lds_barrier();  // B2: D and the image complete; da2 image and a1 slot it&1 consumed
-            PH(1);
             if (it + 1 < nmine) {
                 issued += issue_dy(it + 1);
                 m_dy = issued;
             }
             if (it + 2 < nmine) issued += issue_ax(it + 2, it & 1);
-            PH(4);
-            PH_ITER();
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        PH_FLUSH();
         float* out = slab2 + (size_t)blockIdx.x * 512 * 64;
 #pragma unroll
         for (int t = 0; t < 4; ++t)
@@ -1643,12 +1472,9 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
         const int bd0 = 16 * (si + 128 * g + c2::zc(g));
         const int bd6 = 16 * (min(96 + si, 99) + 128 * g + c2::zc(g));
         float bs8[8] = {};  // !FI_C1B_PH2: conv1 bias partials, channels 8g + j of this lane's da1 pixels
-        PH_DECL
         for (int it = 0; it < nmine; ++it) {
             const int f = frame_of(it);
-            PH(5);
             lds_barrier();  // B1
-            PH(1);
             {  // conv2 data gradient of class (ty, tx) -> D (and da1_out)
                 const char* X = smem + c21::O_AX + (it & 1) * c21::AXB;
                 u32x4* dst = KEEP_DA1 ? (u32x4*)(da1_out + (size_t)f * 12800) : nullptr;
@@ -1721,7 +1547,6 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                     }
                 }
             }
-            PH(2);
 #pragma unroll
             for (int i = 0; i < c21::NRAW_B; ++i) {  // raw(it), the last units -> image
                 const int u = 256 * c21::NRAW_A + t4 + 256 * i;
@@ -1732,9 +1557,7 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                     *(bf16x8*)(IMG + c1::PLANE + 16 * u) = hi;
                 }
             }
-            PH(4);
             lds_barrier();  // B2: D and the image complete
-            PH(1);
             if (it + 1 < nmine) load_raw(it + 1);
             switch (wr) {  // the bias split is compile-time per wave (no branch in the m-step loop)
                 case 0: conv1_wgrad(std::integral_constant<int, 0>{}); break;
@@ -1742,10 +1565,7 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                 case 2: conv1_wgrad(std::integral_constant<int, 2>{}); break;
                 default: conv1_wgrad(std::integral_constant<int, 3>{}); break;
             }
-            PH(3);
-            PH_ITER();
         }
-        PH_FLUSH();
         // conv1 bias partial of this wave: channel lane & 31, the two pixel halves of the B
         // fragments combined
         if constexpr (FI_C1B_PH2) {
@@ -1783,7 +1603,6 @@ int conv21_bwd_fr_launch(const __bf16* a1, const __bf16* da2, const __bf16* w2d,
         hipLaunchKernelGGL(conv21_bwd_fr<false>, dim3(grid), dim3(512), 0, s, a1, da2, w2d, frames, da1_out, slab2,
                            cs2, slab1, cs1, nframes, a1_planar);
     FI_HIP_CHECK(hipGetLastError());
-    ph_report("conv21_bwd", grid);
     return FI_OK;
 }
 
@@ -1930,16 +1749,12 @@ __device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, int nst, W
         if (nmine > 2) issued += issue(2, 0);
         mB = issued;
     }
-    PH_DECL
     for (int it = 0; it < nmine; ++it) {
         const int f = blockIdx.x + it * gridDim.x;
         char* X = smem + (it & 1) * c3::SLOT2;
-        PH(5);
         lds_barrier();  // frame it in slot it&1; every wave done with frame it-1 (slot (it+1)&1)
-        PH(1);
         if (ISSUER && it + 1 < nmine) {
             wait_vmcnt(issued - mA);  // own pieces of frame it+1 landed
-            PH(0);
             reshuffle((it + 1) & 1, (it + 1) & 1);
             int mC = issued;
             if (it + 3 < nmine) {
@@ -1949,14 +1764,10 @@ __device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, int nst, W
             mA = mB;
             mB = mC;
         }
-        PH(2);
         work(X, f);
         issued += nst;
-        PH(3);
-        PH_ITER();
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    PH_FLUSH();
 }
 
 // weight gradient of one wave, taps t = 2i + B (B = wr>>1), i < 5 - B
@@ -2159,8 +1970,6 @@ int conv3_bwd_fr_launch(const __bf16* a2, const __bf16* da3, const __bf16* a3, c
     hipLaunchKernelGGL(conv3_bwd_fr, dim3(grid), dim3(512), 0, s, a2, da3, a3, w3d, da2,
                        slab, cs_slab, cs2, nframes);
     FI_HIP_CHECK(hipGetLastError());
-    st_report("conv3_bwd");
-    ph_report("conv3_bwd", grid);
     return FI_OK;
 }
 

@@ -508,6 +508,216 @@ __global__ __launch_bounds__(64 * VtLayout<A>::NW, VtLayout<A>::WPS) void vtrace
 }
 
 // ------------------------------------------------------------------------------------
+// Kernel 4 (vtrace_stream_kernel<A>): no chain of time chunks. A persistent
+// 512-thread workgroup (one per CU, 132 KB of LDS) walks column GROUPS of 4 batch columns,
+// g = lg, lg + G, ...; a group's whole sequence (pi and mu tiles: T rows x 288 B; act / rew /
+// disc: T rows x 16 B; val: T+1 rows) is DMA'd into one of two slots, and the NEXT group's DMA
+// is issued right after this one landed, so the loads of group g+1 stream while group g is
+// computed and stored. Thread (t, c) = (tid >> 2, tid & 3) owns one (t, b) row:
+//   A  every carry-independent quantity as the slot lands (softmax statistics of pi and mu,
+//      rho, c, pg-rho, delta, gamma c);
+//   B  one affine suffix scan over t per column: butterfly inside the wave (lanes 4, 8, 16, 32
+//      apart hold rows 1, 2, 4, 8 later), wave totals combined through LDS;
+//   C  vs, pg_adv, dvalue and dlogits (written over the thread's own pi row, then stored as
+//      the tile's full 16-B pieces: 288-B row runs, the global layout's).
+// Stores always issue (rows t >= T go to the scratch sink), so every wave issues exactly the
+// same VMEM count per group and the wait for group g+1's DMA leaves group g's stores in flight.
+// Requires T <= 127 (thread row T writes the bootstrap dvalue), B % 4 == 0, even A <= 20.
+// ------------------------------------------------------------------------------------
+template <int A>
+struct VtStr {
+    static constexpr int NC = 4;                        // batch columns per group
+    static constexpr int NT = 512;                      // threads: (t, c) = (tid >> 2, tid & 3)
+    static constexpr int TMAX = NT / NC - 1;            // 127 (thread row T carries the bootstrap dvalue)
+    static constexpr int ROWB = NC * A * 4;             // bytes per t-row of a logits tile (288 at A=18)
+    static constexpr int PPR = ROWB / 16;               // 16-B pieces per t-row
+    static constexpr int NW = NT / 64;                  // 8 waves
+    static constexpr int NST = 4 + 3;                   // stores per wave per group (dlogits + vs/adv/dval)
+    static_assert(A % 2 == 0 && ROWB % 16 == 0, "pieces");
+    __host__ __device__ static constexpr int logp(int T) { return (T * ROWB + 1023) / 1024; }  // pieces per logits tile
+    __host__ __device__ static constexpr int scp(int T) { return (T * 16 + 1023) / 1024; }      // per scalar tile
+    __host__ __device__ static constexpr int valp(int T) { return ((T + 1) * 16 + 1023) / 1024; }
+    __host__ __device__ static constexpr int pieces(int T) { return 2 * logp(T) + 3 * scp(T) + valp(T); }
+    __host__ __device__ static constexpr int slot_bytes(int T) { return 1024 * pieces(T); }
+    __host__ __device__ static constexpr int lds_bytes(int T) { return 2 * slot_bytes(T) + NW * NC * 2 * 4; }
+};
+
+// piece j (< pieces(T)) of group b0's slot: the tensor it comes from and the byte offsets
+template <int A>
+__device__ __forceinline__ void vt_str_issue(const VtRsrc& rs, uint32_t slot_lds, int T, int B, int b0, int w, int lane) {
+    using L = VtStr<A>;
+    const int LP = L::logp(T), SP = L::scp(T), NPc = L::pieces(T);
+    const int per_wave = (NPc + L::NW - 1) / L::NW;
+    for (int i = 0; i < per_wave; ++i) {
+        int j = w + L::NW * i;
+        if (j >= NPc) j = w;  // pad the wave's count: a duplicate of its first piece (same bytes, same place)
+        const int q0 = 16 * lane;
+        if (j < 2 * LP) {  // pi | mu
+            const int jj = j < LP ? j : j - LP;
+            int q = jj * 1024 + q0;
+            if (q >= T * L::ROWB) q = q0 % L::ROWB;  // past the tile: row 0 again, lands in the padding
+            const int t = q / L::ROWB, cb = q - t * L::ROWB;
+            blds16_nt(j < LP ? rs.pi : rs.mu, (uint32_t)((t * B + b0) * A * 4 + cb), slot_lds + 1024u * j);
+        } else {  // act | rew | disc (T rows x 16 B) | val (T + 1 rows)
+            const int k = j - 2 * LP, s = k / SP < 3 ? k / SP : 3;
+            const int jj = k - s * SP, rows = s == 3 ? T + 1 : T;
+            int q = jj * 1024 + q0;
+            if (q >= rows * 16) q = q0 % 16;
+            const int t = q >> 4, cb = q & 15;
+            blds16_nt(s == 0 ? rs.act : s == 1 ? rs.rew : s == 2 ? rs.disc : rs.val,
+                      (uint32_t)((t * B + b0) * 4 + cb), slot_lds + 1024u * j);
+        }
+    }
+}
+
+template <int S>
+__device__ __forceinline__ float vt_shx(float v) { return __shfl_xor(v, S, 64); }
+template <int S>
+__device__ __forceinline__ void vt_str_scan_step(float& sd, float& sg, float& ed, float& eg, int lane) {
+    const float pd = vt_shx<S>(sd), pg = vt_shx<S>(sg);
+    const bool later = (lane & S) == 0;  // the partner segment holds later rows
+    ed = later ? ed + eg * pd : ed;
+    eg = later ? eg * pg : eg;
+    sd = later ? sd + sg * pd : pd + pg * sd;
+    sg = sg * pg;
+}
+
+template <int A>
+__global__ __launch_bounds__(512, 1) void vtrace_stream_kernel(VtArgs a) {
+    using L = VtStr<A>;
+    extern __shared__ __attribute__((aligned(16))) char vsm[];
+    const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
+    const int T = a.T, B = a.B;
+    const int tt = tid >> 2, c = tid & 3;
+    const bool valid = tt < T;
+    const int G = gridDim.x, lg = xcd_remap(blockIdx.x, G);
+    const int ngroups = B / L::NC;
+    const int SB = L::slot_bytes(T), LP = L::logp(T), SP = L::scp(T);
+    const uint32_t lds0 = lds_addr(vsm);
+    float* tot = (float*)(vsm + 2 * SB);  // [NW][NC][2] wave totals
+    const VtRsrc rs = vt_rsrc(a);
+    const fi_vtrace_hparams hp = a.hp;
+    constexpr float L2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
+    float pg = 0.f, base = 0.f, ent = 0.f;
+    float* const sink = a.sink + tid;
+    int k = 0;
+    if (lg < ngroups) vt_str_issue<A>(rs, lds0, T, B, L::NC * lg, w, lane);
+    for (int grp = lg; grp < ngroups; grp += G, ++k) {
+        const int b0 = L::NC * grp, b = b0 + c;
+        char* const sl = vsm + (k & 1) * SB;
+        // this group's pieces landed (the previous group's NST stores may still be in flight)
+        wait_vmcnt(k == 0 ? 0 : L::NST);
+        lds_barrier();  // B1: every wave's pieces landed; the other slot's last reads are done
+        if (grp + G < ngroups) vt_str_issue<A>(rs, lds0 + ((k + 1) & 1) * SB, T, B, L::NC * (grp + G), w, lane);
+
+        // ---- A: carry-independent work of row (tt, b)
+        const int tr = valid ? tt : 0;
+        float* zpi = (float*)(sl + tr * L::ROWB + c * A * 4);
+        const float* zmu = (const float*)(sl + 1024 * LP + tr * L::ROWB + c * A * 4);
+        const int* sact = (const int*)(sl + 2048 * LP);
+        const float* srew = (const float*)(sl + 2048 * LP + 1024 * SP);
+        const float* sdisc = (const float*)(sl + 2048 * LP + 2048 * SP);
+        const float* sval = (const float*)(sl + 2048 * LP + 3072 * SP);
+        f32x2 zp2[A / 2], zm2[A / 2];
+#pragma unroll
+        for (int i = 0; i < A / 2; ++i) {
+            zp2[i] = *(const f32x2*)(zpi + 2 * i);
+            zm2[i] = *(const f32x2*)(zmu + 2 * i);
+        }
+        int at = sact[4 * tr + c];
+        if (valid && (unsigned)at >= (unsigned)A) atomicAdd(a.bad, 1);
+        at = at < 0 ? 0 : (at >= A ? A - 1 : at);
+        const float zpa = zpi[at], zma = zmu[at];
+        const float rw = srew[4 * tr + c], g = sdisc[4 * tr + c], v = sval[4 * tr + c], vn = sval[4 * tr + 4 + c];
+        float mx = vt_max3(zp2[0].x, zp2[0].y, zp2[0].y), mm = vt_max3(zm2[0].x, zm2[0].y, zm2[0].y);
+#pragma unroll
+        for (int i = 1; i < A / 2; ++i) {
+            mx = vt_max3(mx, zp2[i].x, zp2[i].y);
+            mm = vt_max3(mm, zm2[i].x, zm2[i].y);
+        }
+        const f32x2 nmx = {-mx * L2E, -mx * L2E}, nmm = {-mm * L2E, -mm * L2E};
+        f32x2 sp2 = {0.f, 0.f}, sm2 = {0.f, 0.f}, sz2 = {0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < A / 2; ++i) {
+            const f32x2 ap = zp2[i] * L2E + nmx;
+            const f32x2 am = zm2[i] * L2E + nmm;
+            const f32x2 e = f32x2{VT_EXP2(ap.x), VT_EXP2(ap.y)};
+            sp2 += e;
+            sz2 += e * zp2[i];
+            sm2 += f32x2{VT_EXP2(am.x), VT_EXP2(am.y)};
+        }
+        const float sp = sp2.x + sp2.y, sm = sm2.x + sm2.y;
+        const float lse = mx + VT_LOG2(sp) * LN2, lsem = mm + VT_LOG2(sm) * LN2;
+        const float inv = __builtin_amdgcn_rcpf(sp);
+        const float plogp = (sz2.x + sz2.y) * inv - lse;
+        const float lpa = zpa - lse, lma = zma - lsem;
+        const float ratio = VT_EXP(lpa - lma);
+        const float rho = fminf(hp.rho_bar, ratio);
+        const float cc = hp.lambda_ * fminf(hp.c_bar, ratio);
+        const float pgr = fminf(hp.pg_rho_bar, ratio);
+        const float d_own = valid ? rho * (rw + g * vn - v) : 0.f;
+        const float g_own = valid ? g * cc : 1.f;
+
+        // ---- B: reverse affine scan over t (rows 16w .. 16w + 15 of this wave, 4 lanes apart)
+        float sd = d_own, sg = g_own, ed = 0.f, eg = 1.f;
+        vt_str_scan_step<4>(sd, sg, ed, eg, lane);
+        vt_str_scan_step<8>(sd, sg, ed, eg, lane);
+        vt_str_scan_step<16>(sd, sg, ed, eg, lane);
+        vt_str_scan_step<32>(sd, sg, ed, eg, lane);
+        if (lane < L::NC) {
+            tot[(w * L::NC + c) * 2] = sd;
+            tot[(w * L::NC + c) * 2 + 1] = sg;
+        }
+        lds_barrier();  // B2: wave totals visible
+        float acc_in = 0.f;  // acc at row 16(w + 1): the later waves composed onto acc_T = 0
+#pragma unroll
+        for (int w2 = L::NW - 1; w2 > 0; --w2)
+            if (w2 > w) acc_in = tot[(w2 * L::NC + c) * 2] + tot[(w2 * L::NC + c) * 2 + 1] * acc_in;
+        const float acc_nx = ed + eg * acc_in;
+        const float acc = d_own + g_own * acc_nx;
+
+        // ---- C: targets, gradients, stores
+        const float vs_t = v + acc;
+        const float vs_n = vn + acc_nx;
+        const float adv = pgr * (rw + g * vs_n - v);
+        const float dv = -hp.baseline_cost * acc;
+        {  // dlogits over this thread's own pi row
+            const float ec = hp.entropy_cost;
+            const float al = inv * (adv - ec * (plogp + lse)), be = inv * ec;
+            const f32x2 al2 = {al, al};
+#pragma unroll
+            for (int i = 0; i < A / 2; ++i) {
+                const f32x2 ap = zp2[i] * L2E + nmx;
+                const f32x2 e = f32x2{VT_EXP2(ap.x), VT_EXP2(ap.y)};
+                if (valid) *(f32x2*)(zpi + 2 * i) = e * (zp2[i] * be + al2);
+            }
+            if (valid) zpi[at] -= adv;
+        }
+        if (valid) {
+            pg += -adv * lpa;
+            base += 0.5f * acc * acc;
+            ent += plogp;
+        }
+        {  // vs / pg_adv / dvalue of the thread's row; thread row T writes the bootstrap dvalue 0
+            const size_t e = (size_t)tt * B + b;
+            VT_ST(vs_t, valid ? a.vs + e : sink);
+            VT_ST(adv, valid ? a.adv + e : sink);
+            VT_ST(valid ? dv : 0.f, tt <= T ? a.dval + e : sink);
+        }
+        lds_barrier();  // B3: the dlogits rows are complete
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {  // the tile's T * PPR pieces, 4 rounds of 512
+            const int q = L::NT * i + tid;
+            const int row = q / L::PPR, pc = q - row * L::PPR;
+            const f32x4 d4 = *(const f32x4*)(sl + 16 * (q < T * L::PPR ? q : 0));
+            VT_ST(d4, q < T * L::PPR ? (f32x4*)(a.dlog + (size_t)(row * B + b0) * A) + pc : (f32x4*)(a.sink + 4 * tid));
+        }
+    }
+    __syncthreads();
+    block_reduce3((double)pg, (double)base, (double)ent, (double*)vsm, a.part + (size_t)blockIdx.x * 3);
+}
+
+// ------------------------------------------------------------------------------------
 // Kernel 3 (vtrace_seq_kernel<A>, on request only -- measured slower than kernel 1, DESIGN.md
 // section 5): a persistent 256-thread
 // workgroup walks column PAIRS p = lg, lg + G, ... and owns each pair for the WHOLE sequence,
@@ -622,28 +832,20 @@ __global__ __launch_bounds__(256, 2) void vtrace_seq_kernel(VtArgs a) {
     const int np = T * L::PPR;
     int n_dl = 0;
     for (int i = w; 64 * i < np; i += 4) ++n_dl;
-#ifdef FI_VTS_NOSTORE  // timing experiment: no output stores
-    const int n_st = 0;
-#else
     const int n_st = 3 + n_dl;
-#endif
     float pg = 0.f, base = 0.f, ent = 0.f;
     float* const sink = a.sink + tid;  // stores of lanes with t >= T
 
     int k = 0;
     int p = lg;
-#ifndef FI_VTS_NODMA
     if (p < npairs) vt_seq_issue<A>(rs, lds0, T, B, w, lane, L::NB * p);
-#endif
     for (; p < npairs; p += G, ++k) {
         const int b0 = L::NB * p, b = b0 + c;
         char* const sl = vsm + (k & 1) * SB;
         // this pair's DMA landed (the previous pair's stores may still be in flight)
         wait_vmcnt(k > 0 ? n_st : 0);
         lds_barrier();  // B1: slot k&1 landed for every wave; slot (k+1)&1's last reads done
-#ifndef FI_VTS_NODMA  // timing experiment: no input DMA (the slots hold whatever is there)
         if (p + G < npairs) vt_seq_issue<A>(rs, lds0 + ((k + 1) & 1) * SB, T, B, w, lane, L::NB * (p + G));
-#endif
         if (tid < L::NB) a.dval[(size_t)T * B + b0 + tid] = 0.f;  // the bootstrap row (not counted: see below)
 
         // scalars of the lane's (t, b)
@@ -651,11 +853,7 @@ __global__ __launch_bounds__(256, 2) void vtrace_seq_kernel(VtArgs a) {
         const float* srew = (const float*)(sl + 2 * L::tile_bytes(T) + L::col_bytes(T));
         const float* sdisc = (const float*)(sl + 2 * L::tile_bytes(T) + 2 * L::col_bytes(T));
         const float* sval = (const float*)(sl + 2 * L::tile_bytes(T) + 3 * L::col_bytes(T));
-#ifdef FI_VTS_NODMA
-        int at = sact[2 * tt + c] & 7;
-#else
         int at = sact[2 * tt + c];
-#endif
         const float rw = srew[2 * tt + c], g = sdisc[2 * tt + c], v = sval[2 * tt + c], vn = sval[2 * tt + 2 + c];
         if (valid && (unsigned)at >= (unsigned)A) atomicAdd(a.bad, 1);
         at = at < 0 ? 0 : (at >= A ? A - 1 : at);
@@ -667,13 +865,8 @@ __global__ __launch_bounds__(256, 2) void vtrace_seq_kernel(VtArgs a) {
         f32x2 zp2[A / 2], zm2[A / 2];
 #pragma unroll
         for (int i = 0; i < A / 2; ++i) {
-#ifdef FI_VTS_NOCOMP  // timing experiment: no logits reads (softmax on constants)
-            zp2[i] = f32x2{0.f, (float)i};
-            zm2[i] = f32x2{(float)i, 0.f};
-#else
             zp2[i] = *(const f32x2*)(zpi + 2 * i);
             zm2[i] = *(const f32x2*)(zmu + 2 * i);
-#endif
         }
         const float zpa = zpi[at], zma = zmu[at];
         float mx = vt_max3(zp2[0].x, zp2[0].y, zp2[0].y), mm = vt_max3(zm2[0].x, zm2[0].y, zm2[0].y);
@@ -750,20 +943,15 @@ __global__ __launch_bounds__(256, 2) void vtrace_seq_kernel(VtArgs a) {
             base += 0.5f * acc * acc;
             ent += plogp;
         }
-#ifndef FI_VTS_NOSTORE
         {  // every lane stores (the sink takes rows t >= T), so each wave issues exactly 3 here
             const size_t e = (size_t)tt * B + b;
             VT_ST(vs_t, valid ? a.vs + e : sink);
             VT_ST(adv, valid ? a.adv + e : sink);
             VT_ST(dv, valid ? a.dval + e : sink);
         }
-#else
-        asm volatile("" ::"v"(vs_t), "v"(adv), "v"(dv));
-#endif
         lds_barrier();  // B3: the slot's dlogits rows complete
 
         // the dlogits tile out in the global layout (144-B runs), 16 B per lane
-#ifndef FI_VTS_NOSTORE
         for (int i = w; 64 * i < np; i += 4) {
             const int q = 64 * i + lane;
             if (q < np) {
@@ -772,7 +960,6 @@ __global__ __launch_bounds__(256, 2) void vtrace_seq_kernel(VtArgs a) {
                 VT_ST(d4, (f32x4*)(a.dlog + (size_t)(row * B + b0) * A) + pc);
             }
         }
-#endif
         // the bootstrap-row store above is the one VMEM op not in n_st: it was issued BEFORE
         // this pair's stores, i.e. it is older than them and retired by the next wait as well
     }
@@ -834,6 +1021,22 @@ static int seq_grid(int B) {
 
 static bool lds_supported(int A, int B) { return B % 8 == 0 && A % 2 == 0 && A >= 2 && A <= 20; }
 
+template <int A>
+static void launch_str(const VtArgs& a, int nblk, hipStream_t s) {
+    hipLaunchKernelGGL(vtrace_stream_kernel<A>, dim3(nblk), dim3(VtStr<A>::NT), VtStr<A>::lds_bytes(a.T), s, a);
+}
+// persistent grid of the streaming kernel: one workgroup per CU (132 KB of LDS at T = 100)
+static int str_grid(int B) {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess)
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    return std::max(1, std::min(B / 4, cus));
+}
+static bool str_supported(int T, int A, int B) {
+    return B % 4 == 0 && A % 2 == 0 && A >= 2 && A <= 20 && T <= VtStr<2>::TMAX &&
+           VtStr<20>::lds_bytes(T) <= 160 * 1024;
+}
+
 int vtrace_launch(int variant, int T, int B, int A, const float* pi, const float* mu,
                   const int32_t* act, const float* rew, const float* disc, const float* val,
                   const fi_vtrace_hparams& hp, float* vs, float* adv, float* dlog, float* dval,
@@ -877,6 +1080,31 @@ int vtrace_launch(int variant, int T, int B, int A, const float* pi, const float
             case 16: launch_seq<16>(a, nblk, stream); break;
             case 18: launch_seq<18>(a, nblk, stream); break;
             case 20: launch_seq<20>(a, nblk, stream); break;
+            default: return fail(FI_ERR_UNSUPPORTED, "vtrace: A not instantiated");
+        }
+        FI_HIP_CHECK(hipGetLastError());
+        if (nblk_out) *nblk_out = nblk;
+        if (finalize) return vtrace_finalize_launch(ws, nblk, losses, stream, a.bad);
+        return FI_OK;
+    }
+    if (variant == 4) {
+        FI_REQUIRE(str_supported(T, A, B) && fits32, "vtrace: streaming kernel needs T<=127, B%4==0, even A<=20");
+        FI_REQUIRE(vs && adv, "vtrace: streaming kernel writes vs and pg_adv (non-null)");
+        FI_REQUIRE(((uintptr_t)pi | (uintptr_t)mu | (uintptr_t)dlog) % 16 == 0 &&
+                   ((uintptr_t)act | (uintptr_t)rew | (uintptr_t)disc | (uintptr_t)val) % 16 == 0,
+                   "vtrace: streaming kernel needs 16-byte aligned tensors");
+        const int nblk = str_grid(B);
+        switch (A) {
+            case 2: launch_str<2>(a, nblk, stream); break;
+            case 4: launch_str<4>(a, nblk, stream); break;
+            case 6: launch_str<6>(a, nblk, stream); break;
+            case 8: launch_str<8>(a, nblk, stream); break;
+            case 10: launch_str<10>(a, nblk, stream); break;
+            case 12: launch_str<12>(a, nblk, stream); break;
+            case 14: launch_str<14>(a, nblk, stream); break;
+            case 16: launch_str<16>(a, nblk, stream); break;
+            case 18: launch_str<18>(a, nblk, stream); break;
+            case 20: launch_str<20>(a, nblk, stream); break;
             default: return fail(FI_ERR_UNSUPPORTED, "vtrace: A not instantiated");
         }
         FI_HIP_CHECK(hipGetLastError());

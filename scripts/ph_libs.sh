@@ -1,5 +1,6 @@
 #!/bin/bash
 # per-phase clocks + per-kernel ms of several FI_PHASES experiment builds (build/exp/lib_NAME.so)
+# (the instrumentation lives in scripts/patches/atari_fr_phase_clocks.patch: apply it first)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 for L in ${LIBS:-ph}; do
