@@ -80,7 +80,7 @@ def host_cpu_info():
             "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
 
 
-def cpu_baseline(arch, T, A, seconds, threads):
+def cpu_baseline(arch, T, A, seconds, threads, full=False):
     """Time a CPU learner step on rank 0 (test infrastructure under oracle/, kind 'port'):
     the torch-CPU port of the step (oracle/torch_learner.py: oneDNN/MKL fp32 convolutions and
     GEMMs, autograd, the same V-trace/loss/clip/Adam as the C oracle; gradient-equal to it,
@@ -116,6 +116,12 @@ def cpu_baseline(arch, T, A, seconds, threads):
                   f"T={T}, full B=4096 (min of 2 steps, {per_b[4096]:.2f} s; B=512: {per_b[512]:.3f} s "
                   f"= {T * 512 / per_b[512]:.0f} env-steps/s)")
         extrap = False
+    elif full:  # --cpu-full: one whole T x 4096 step (~1 min, ~150 GB of host memory)
+        Bs = 4096
+        step = one(Bs)
+        sample = (f"torch-CPU port of the Atari-net learner step (fwd+vtrace+bwd+clip+adam, fp32), "
+                  f"T={T}, the full B=4096 (one step, {step:.1f} s)")
+        extrap = False
     else:
         t = one(2)
         target = max(1.0, seconds / 3.0)
@@ -123,7 +129,7 @@ def cpu_baseline(arch, T, A, seconds, threads):
         step = min(one(Bs) for _ in range(2))
         sample = (f"torch-CPU port of the Atari-net learner step (fwd+vtrace+bwd+clip+adam, fp32), "
                   f"T={T}, B={Bs} per step (min of 2 steps, {step:.2f} s each); EXTRAPOLATED to "
-                  f"B=4096 as env-steps/s flat in B")
+                  f"B=4096 as env-steps/s flat in B (a full B=4096 step: bench.py --cpu-full)")
         extrap = Bs < 4096
     # V-trace + loss + grads alone at the full config size (the C oracle)
     case = orc.synth_batch(7, T=T, B=4096, A=A, D=1, obs=False)
@@ -153,6 +159,8 @@ def main():
     ap.add_argument("--profile-steps", type=int, default=3)
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-full", action="store_true",
+                    help="time one whole T x 4096 CPU step for cpu_baseline (Atari: ~1 min, ~150 GB host memory)")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
@@ -285,7 +293,7 @@ def main():
         # on the pool's boxes, whose nproc counts the whole host), else the affinity mask
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or host_cpu_info()["affinity_cpus"] or 1
         try:
-            result["cpu_baseline"] = cpu_baseline(args.arch, T, A, args.cpu_seconds, threads)
+            result["cpu_baseline"] = cpu_baseline(args.arch, T, A, args.cpu_seconds, threads, full=args.cpu_full)
             result["cpu_baseline"]["threads_basis"] = (
                 "OMP_NUM_THREADS from the environment: the pool gives one GPU's job a 16-CPU share and "
                 "sets OMP_NUM_THREADS=16 (nproc / the affinity mask count the whole host, shared with "

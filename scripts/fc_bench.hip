@@ -84,11 +84,17 @@ int main(int argc, char** argv) {
     FWDV("256x256 w4x2 bk32 ns3 prio", 256, 256, 4, 2, 32, 3, 1);
     FWDV("256x256 w4x2 bk32 ns4 prio", 256, 256, 4, 2, 32, 4, 1);
     FWDV("256x256 w4x2 bk32 ns4 prio ntY", 256, 256, 4, 2, 32, 4, 1 | 8);
+    FWDV("256x256 w4x2 bk32 ns4 prio pf", 256, 256, 4, 2, 32, 4, 1 | 64);
+    FWDV("256x256 w2x2 bk32 ns4 pf agpr", 256, 256, 2, 2, 32, 4, 4 | 64);
+    FWDV("256x256 w2x2 bk32 ns4 agpr", 256, 256, 2, 2, 32, 4, 4);
+    FWDV("256x256 w2x2 bk64 ns2 agpr", 256, 256, 2, 2, 64, 2, 4);
     DGV("224x256 w1x8 bk64 ns2 prio", 224, 256, 1, 8, 64, 2, 1);
     DGV("224x256 w1x8 bk64 ns2 prio iss@frag", 224, 256, 1, 8, 64, 2, 1 | 16);
     DGV("224x256 w1x8 bk64 ns2 prio iss@mid", 224, 256, 1, 8, 64, 2, 1 | 32);
     DGV("224x256 w1x8 bk32 ns3 prio", 224, 256, 1, 8, 32, 3, 1);
     DGV("224x256 w1x8 bk32 ns4 prio", 224, 256, 1, 8, 32, 4, 1);
+    DGV("224x256 w1x8 bk32 ns4 prio pf", 224, 256, 1, 8, 32, 4, 1 | 64);
+    DGV("224x256 w2x4 bk32 ns4 prio pf", 224, 256, 2, 4, 32, 4, 1 | 64);
     DGV("224x256 w1x8 bk64 ns2 prio ntst", 224, 256, 1, 8, 64, 2, 1 | 2);
     WGV("256x224 w4x2 bk64 ns2", 9, 256, 224, 4, 2, 64, 2);
     // hipBLASLt (the default fwd / dgrad today), own output buffers: not bit-comparable
