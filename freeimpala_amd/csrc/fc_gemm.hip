@@ -170,7 +170,8 @@ __device__ __forceinline__ int nt_chunk(int c, int row) {
 // OPT bits: 1 = s_setprio 1 around each MFMA cluster, 2 = nontemporal (streaming) output stores,
 // 4 = accumulators in AGPRs (for 4-wave tiles of 128 x 128 per wave), 8 = non-temporal loads of
 // the Y operand (the frame rows), 16 = the next step's DMA issued after the first sub-step's
-// fragment reads (their LDS latency overlaps the issue), 32 = ... after the first sub-step's MFMAs
+// fragment reads (their LDS latency overlaps the issue), 32 = ... after the first sub-step's MFMAs,
+// 64 = LDS-read prefetch across the barrier (BK 32, NS >= 4; see the branch below)
 template <int BX, int BY, int WX, int WY, int BK, int NS, class Epi, int OPT = 0>
 __global__ __launch_bounds__(64 * WX * WY) void fc_nt_kernel(const __bf16* __restrict__ X, const __bf16* __restrict__ Y,
                                                     int NY, int K, int ntx, int ntiles, Epi epi) {
@@ -221,6 +222,77 @@ __global__ __launch_bounds__(64 * WX * WY) void fc_nt_kernel(const __bf16* __res
     };
 
     for (int d = 0; d < D && d < total; ++d) issue(d);
+    if constexpr (OPT & 64) {
+        // LDS-read prefetch across the barrier (BK = 32, NS >= 4): at barrier(it) step it + 1
+        // has landed too, so its fragments are read while step it's MFMAs (fragments already in
+        // registers) run -- the matrix pipe starts right after the barrier. Step it + D goes into
+        // the slot of step it - 1, whose fragments were read before barrier(it - 1).
+        static_assert(BK == 32 && NS >= 4, "prefetch ring");
+        auto frags = [&](int step, bf16x8* fa, bf16x8* fb) {
+            const char* sx = lds + (step % NS) * SLOT;
+            const char* sy = sx + BX * BK * 2;
+#pragma unroll
+            for (int f = 0; f < FX; ++f) {
+                const int row = wx * TX + f * 16 + (lane & 15);
+                fa[f] = *(const bf16x8*)(sx + row * (BK * 2) + (nt_chunk<BK>(G, row) << 4));
+            }
+#pragma unroll
+            for (int g = 0; g < FY; ++g) {
+                const int row = wy * TY + g * 16 + (lane & 15);
+                fb[g] = *(const bf16x8*)(sy + row * (BK * 2) + (nt_chunk<BK>(G, row) << 4));
+            }
+        };
+        bf16x8 ca[FX], cb[FY];
+        vm_wait_rt(min(D - 1, total - 1) * PW);
+        lds_barrier();
+        if (total > 0) frags(0, ca, cb);
+        const int mytiles = total / nk;
+        int it = 0, last_epi = -(1 << 20);
+        for (int tile_it = 0; tile_it < mytiles; ++tile_it) {
+            f32x4 acc[FX][FY];
+#pragma unroll
+            for (int f = 0; f < FX; ++f)
+#pragma unroll
+                for (int g = 0; g < FY; ++g) acc[f][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int kt = 0; kt < nk; ++kt, ++it) {
+                bf16x8 na[FX], nb[FY];
+                if (it + 1 < total) {
+                    // younger than step it + 1's pieces: steps it + 2 .. it + D - 1, and an
+                    // epilogue issued after step it + 1's DMA (iteration >= it + 1 - D)
+                    vm_wait_rt(max(0, min(D - 2, total - 2 - it)) * PW + (last_epi >= it + 1 - D ? NST : 0));
+                    lds_barrier();
+                    if (it + D < total) issue(it + D);
+                    frags(it + 1, na, nb);
+                }
+                if constexpr (OPT & 1) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+                for (int f = 0; f < FX; ++f)
+#pragma unroll
+                    for (int g = 0; g < FY; ++g)
+                        acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ca[f], cb[g], acc[f][g], 0, 0, 0);
+                if constexpr (OPT & 1) __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+                for (int f = 0; f < FX; ++f) ca[f] = na[f];
+#pragma unroll
+                for (int g = 0; g < FY; ++g) cb[g] = nb[g];
+            }
+            const int t = lg + tile_it * NG;
+            const int ty = t / ntx, tx = t - ty * ntx;
+            const int y0 = ty * BY;
+            const OutTile ot = epi.tile(y0, min(BY, NY - y0));
+            const int xw = tx * BX + wx * TX, yb = y0 + wy * TY + (lane & 15);
+#pragma unroll
+            for (int g = 0; g < FY; ++g) {
+#pragma unroll
+                for (int f = 0; f + 1 < FX; f += 2)
+                    Epi::template pair<AUX>(ot, lb, xw + f * 16, yb + g * 16, G, acc[f][g], acc[f + 1][g]);
+                if constexpr (FX % 2)
+                    Epi::template single<AUX>(ot, lb, xw + (FX - 1) * 16, yb + g * 16, G, acc[FX - 1][g]);
+            }
+            last_epi = it - 1;
+        }
+        return;
+    }
     // tile-outer / k-inner: the accumulators are zeroed per tile outside the k loop (a reset
     // inside it would merge two definitions at the loop head: with AGPR accumulators the
     // compiler then copies every accumulator through VGPRs each step)
@@ -397,11 +469,12 @@ __global__ __launch_bounds__(512) void fc_tn_kernel(const __bf16* __restrict__ X
 
 #ifndef FI_FC_CONFIG_OVERRIDE
 // (BX, BY, WX, WY, BK, NS[, OPT]) chosen with scripts/fc_bench.hip (interleaved A/B at R = 413,696)
-// forward: 256 output columns x 256 rows, waves 4 (x) x 2 (y), 2 slots of k 64, s_setprio
-#define FC_FW_CFG 256, 256, 4, 2, 64, 2, 1
+// forward: 256 output columns x 256 rows, waves 4 (x) x 2 (y), 2 slots of k 64, s_setprio, the
+// next step's DMA issued after the first fragment reads (round 4: 1.257 -> 1.225 ms)
+#define FC_FW_CFG 256, 256, 4, 2, 64, 2, 1 | 16
 // dgrad: 3136 = 14 x 224 output columns, 256 rows, waves 1 x 8 (14 x 2 fragments per wave),
-// s_setprio
-#define FC_DG_CFG 224, 256, 1, 8, 64, 2, 1
+// s_setprio, non-temporal da3 stores (round 4: 1.652 -> 1.591 ms)
+#define FC_DG_CFG 224, 256, 1, 8, 64, 2, 1 | 2
 // wgrad: x = dh columns (2 x 256), y = a3 columns (14 x 224), waves 4 x 2
 #define FC_WG_CFG 256, 224, 4, 2, 64, 2
 #endif

@@ -32,6 +32,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <mutex>
 
 namespace fi {
 
@@ -1023,6 +1024,12 @@ static bool lds_supported(int A, int B) { return B % 8 == 0 && A % 2 == 0 && A >
 
 template <int A>
 static void launch_str(const VtArgs& a, int nblk, hipStream_t s) {
+    // more than 64 KB of dynamic LDS: raise the kernel's limit once (thread-safe, per instantiation)
+    static std::once_flag once;
+    std::call_once(once, [] {
+        (void)hipFuncSetAttribute((const void*)vtrace_stream_kernel<A>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+    });
     hipLaunchKernelGGL(vtrace_stream_kernel<A>, dim3(nblk), dim3(VtStr<A>::NT), VtStr<A>::lds_bytes(a.T), s, a);
 }
 // persistent grid of the streaming kernel: one workgroup per CU (132 KB of LDS at T = 100)
@@ -1032,9 +1039,13 @@ static int str_grid(int B) {
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     return std::max(1, std::min(B / 4, cus));
 }
+// (the two slots hold the whole sequence of a group: T <= 124 at A = 18 within 160 KB of LDS)
+static int str_lds_bytes(int T, int A) {
+    const int logp = (T * 4 * A * 4 + 1023) / 1024, scp = (T * 16 + 1023) / 1024, valp = ((T + 1) * 16 + 1023) / 1024;
+    return 2 * 1024 * (2 * logp + 3 * scp + valp) + 8 * 4 * 2 * 4;
+}
 static bool str_supported(int T, int A, int B) {
-    return B % 4 == 0 && A % 2 == 0 && A >= 2 && A <= 20 && T <= VtStr<2>::TMAX &&
-           VtStr<20>::lds_bytes(T) <= 160 * 1024;
+    return B % 4 == 0 && A % 2 == 0 && A >= 2 && A <= 20 && T <= VtStr<2>::TMAX && str_lds_bytes(T, A) <= 160 * 1024;
 }
 
 int vtrace_launch(int variant, int T, int B, int A, const float* pi, const float* mu,
@@ -1088,7 +1099,8 @@ int vtrace_launch(int variant, int T, int B, int A, const float* pi, const float
         return FI_OK;
     }
     if (variant == 4) {
-        FI_REQUIRE(str_supported(T, A, B) && fits32, "vtrace: streaming kernel needs T<=127, B%4==0, even A<=20");
+        FI_REQUIRE(str_supported(T, A, B) && fits32,
+                   "vtrace: streaming kernel needs B%4==0, even A<=20 and the whole sequence of 4 columns in 80 KB of LDS");
         FI_REQUIRE(vs && adv, "vtrace: streaming kernel writes vs and pg_adv (non-null)");
         FI_REQUIRE(((uintptr_t)pi | (uintptr_t)mu | (uintptr_t)dlog) % 16 == 0 &&
                    ((uintptr_t)act | (uintptr_t)rew | (uintptr_t)disc | (uintptr_t)val) % 16 == 0,

@@ -4,8 +4,8 @@
 // GEMM (same k order per output element, so the results must be identical).
 // Build: scripts/build_fc_bench.sh; run: build/fc_bench [rounds]
 #define FI_FC_CONFIG_OVERRIDE
-#define FC_FW_CFG 256, 256, 4, 2, 64, 2, 1
-#define FC_DG_CFG 224, 256, 1, 8, 64, 2, 1
+#define FC_FW_CFG 256, 256, 4, 2, 64, 2, 1 | 16
+#define FC_DG_CFG 224, 256, 1, 8, 64, 2, 1 | 2
 #define FC_WG_CFG 256, 224, 4, 2, 64, 2
 #include "../freeimpala_amd/csrc/fc_gemm.hip"
 #include "../freeimpala_amd/csrc/fc_blaslt.h"
