@@ -75,27 +75,21 @@ int main(int argc, char** argv) {
     };
 #define FWDV(nm, ...) add("fwd  " nm, 0, [&](hipStream_t st, int k) { return fc_fwd_impl<__VA_ARGS__>(a3, wT, bias, h[k], R, st); }, h[0], h[1], (size_t)R * FCO * 2)
 #define DGV(nm, ...) add("dgrd " nm, 1, [&](hipStream_t st, int k) { return fc_dgrad_impl<__VA_ARGS__>(dh, w, da3[k], R, st); }, da3[0], da3[1], (size_t)R * FCK * 2)
+#define FWSV(nm, ...) add("fwd  " nm, 0, [&](hipStream_t st, int k) { return fc_fwd_ws_impl<__VA_ARGS__>(a3, wT, bias, h[k], R, st); }, h[0], h[1], (size_t)R * FCO * 2)
+#define DGSV(nm, ...) add("dgrd " nm, 1, [&](hipStream_t st, int k) { return fc_dgrad_ws_impl<__VA_ARGS__>(dh, w, da3[k], R, st); }, da3[0], da3[1], (size_t)R * FCK * 2)
 #define WGV(nm, S, ...) add("wgrd " nm, 2, [&](hipStream_t st, int k) { return fc_wgrad_impl<__VA_ARGS__>(a3, dh, slab, dw[k], R, st, S); }, dw[0], dw[1], (size_t)FCK * FCO * 4)
     // the shipped configurations first (fc_gemm.hip FC_*_CFG), then alternatives
-    FWDV("256x256 w4x2 bk64 ns2 prio", 256, 256, 4, 2, 64, 2, 1);
-    FWDV("256x256 w4x2 bk64 ns2 prio ntY", 256, 256, 4, 2, 64, 2, 1 | 8);
     FWDV("256x256 w4x2 bk64 ns2 prio iss@frag", 256, 256, 4, 2, 64, 2, 1 | 16);
-    FWDV("256x256 w4x2 bk64 ns2 prio iss@mid", 256, 256, 4, 2, 64, 2, 1 | 32);
-    FWDV("256x256 w4x2 bk32 ns3 prio", 256, 256, 4, 2, 32, 3, 1);
-    FWDV("256x256 w4x2 bk32 ns4 prio", 256, 256, 4, 2, 32, 4, 1);
-    FWDV("256x256 w4x2 bk32 ns4 prio ntY", 256, 256, 4, 2, 32, 4, 1 | 8);
-    FWDV("256x256 w4x2 bk32 ns4 prio pf", 256, 256, 4, 2, 32, 4, 1 | 64);
-    FWDV("256x256 w2x2 bk32 ns4 pf agpr", 256, 256, 2, 2, 32, 4, 4 | 64);
-    FWDV("256x256 w2x2 bk32 ns4 agpr", 256, 256, 2, 2, 32, 4, 4);
-    FWDV("256x256 w2x2 bk64 ns2 agpr", 256, 256, 2, 2, 64, 2, 4);
-    DGV("224x256 w1x8 bk64 ns2 prio", 224, 256, 1, 8, 64, 2, 1);
-    DGV("224x256 w1x8 bk64 ns2 prio iss@frag", 224, 256, 1, 8, 64, 2, 1 | 16);
-    DGV("224x256 w1x8 bk64 ns2 prio iss@mid", 224, 256, 1, 8, 64, 2, 1 | 32);
-    DGV("224x256 w1x8 bk32 ns3 prio", 224, 256, 1, 8, 32, 3, 1);
-    DGV("224x256 w1x8 bk32 ns4 prio", 224, 256, 1, 8, 32, 4, 1);
-    DGV("224x256 w1x8 bk32 ns4 prio pf", 224, 256, 1, 8, 32, 4, 1 | 64);
-    DGV("224x256 w2x4 bk32 ns4 prio pf", 224, 256, 2, 4, 32, 4, 1 | 64);
+    FWDV("256x256 w4x2 bk64 ns2 ntY midbar", 256, 256, 4, 2, 64, 2, 8 | 4096);
+    FWSV("ws 256x128 c2x2 l4", 256, 128, 2, 2, 4, 0);
+    FWSV("ws 256x128 c2x2 l4 lprio", 256, 128, 2, 2, 4, 1);
+    FWSV("ws 256x128 c2x2 l4 ntY", 256, 128, 2, 2, 4, 8);
+    FWSV("ws 128x256 c2x2 l4", 128, 256, 2, 2, 4, 0);
+    FWSV("ws 256x128 c2x2 l2", 256, 128, 2, 2, 2, 0);
     DGV("224x256 w1x8 bk64 ns2 prio ntst", 224, 256, 1, 8, 64, 2, 1 | 2);
+    DGSV("ws 224x128 c2x2 l4 ntst", 224, 128, 2, 2, 4, 2);
+    DGSV("ws 224x128 c1x4 l4 ntst", 224, 128, 1, 4, 4, 2);
+    DGSV("ws 224x128 c2x2 l4 ntst lprio", 224, 128, 2, 2, 4, 3);
     WGV("256x224 w4x2 bk64 ns2", 9, 256, 224, 4, 2, 64, 2);
     // hipBLASLt (the default fwd / dgrad today), own output buffers: not bit-comparable
     __bf16 *hb, *db;
