@@ -171,14 +171,10 @@ __device__ __forceinline__ int nt_chunk(int c, int row) {
 // 4 = accumulators in AGPRs (for 4-wave tiles of 128 x 128 per wave), 8 = non-temporal loads of
 // the Y operand (the frame rows), 16 = the next step's DMA issued after the first sub-step's
 // fragment reads (their LDS latency overlaps the issue), 32 = ... after the first sub-step's MFMAs,
-// 64 = LDS-read prefetch across the barrier (BK 32, NS >= 4; see the branch below), 128 = the
-// next step's DMA pieces issued one per MPP MFMAs (pinned by sched_barrier) instead of in a block,
-// 256 = two resident workgroups per CU (4-wave tiles, <= 80 KB LDS): each one's barrier bubble is
-// covered by the other's MFMAs on the same SIMDs (grid 2 x 256, registers capped at 256 per wave),
-// 4096 = one barrier per step, between its two halves (BK 64, NS 2; see the branch below), 8192 =
-// (with 4096) the DMA issued after the next half's fragment reads
+// 64 = LDS-read prefetch across the barrier (BK 32, NS >= 4; see the branch below), 4096 = one
+// barrier per step, between its two halves (BK 64, NS 2; see the branch below)
 template <int BX, int BY, int WX, int WY, int BK, int NS, class Epi, int OPT = 0>
-__global__ __launch_bounds__(64 * WX * WY) __attribute__((amdgpu_waves_per_eu((OPT & 256) ? 2 : 1))) void fc_nt_kernel(const __bf16* __restrict__ X, const __bf16* __restrict__ Y,
+__global__ __launch_bounds__(64 * WX * WY) void fc_nt_kernel(const __bf16* __restrict__ X, const __bf16* __restrict__ Y,
                                                     int NY, int K, int ntx, int ntiles, Epi epi) {
     constexpr int TX = BX / WX, TY = BY / WY, FX = TX / 16, FY = TY / 16;
     constexpr int RPP = 1024 / (BK * 2);                      // image rows per 1-KiB DMA piece
@@ -202,43 +198,29 @@ __global__ __launch_bounds__(64 * WX * WY) __attribute__((amdgpu_waves_per_eu((O
     epi.init((float*)(lds + NS * SLOT), threadIdx.x, 64 * NW);
 
     int is_tile = 0, is_kt = 0;  // the next step to issue (tile index of this workgroup, k-step)
-    // a step's operand descriptors and LDS slot (issue_begin), piece i (< PW) of this wave's share
-    // (issue_piece), and the advance to the next step (issue_end); issue = all three
-    struct IssueState {
-        fi_i32x4 rx, ry;
-        int koff;
-        uint32_t sb;
-    };
-    auto issue_begin = [&](int it) {
+    auto issue = [&](int it) {   // this wave's 1-KiB pieces of step `it` into slot it % NS
         const int t = lg + is_tile * NG;
         const int ty = t / ntx, tx = t - ty * ntx;
         const int x0 = tx * BX, y0 = ty * BY;
-        return IssueState{make_rsrc(X + (size_t)x0 * K, (uint32_t)BX * K * 2),
-                          make_rsrc(Y + (size_t)y0 * K, (uint32_t)min(BY, NY - y0) * K * 2), is_kt * BK,
-                          lbase + (uint32_t)(it % NS) * SLOT};
-    };
-    auto issue_piece = [&](const IssueState& st, int i) {
-        int pi = w + NW * i;
-        if (pi >= P) pi -= NW;  // uneven piece count: a duplicate (same bytes, same place)
-        const bool isx = pi < PX;
-        const int prow = (isx ? pi : pi - PX) * RPP + lane / (BK / 8);
-        const int ch = nt_chunk<BK>(lane % (BK / 8), prow);
-        const uint32_t voff = (uint32_t)((prow * K + st.koff + ch * 8) * 2), dst = st.sb + (uint32_t)pi * 1024u;
-        if constexpr (OPT & 8) {
-            if (isx) dma16(st.rx, voff, dst);
-            else dma16_nt(st.ry, voff, dst);
-        } else {
-            dma16(isx ? st.rx : st.ry, voff, dst);
-        }
-    };
-    auto issue_end = [&]() {
-        if (++is_kt == nk) is_kt = 0, ++is_tile;
-    };
-    auto issue = [&](int it) {
-        const IssueState st = issue_begin(it);
+        const fi_i32x4 rx = make_rsrc(X + (size_t)x0 * K, (uint32_t)BX * K * 2);
+        const fi_i32x4 ry = make_rsrc(Y + (size_t)y0 * K, (uint32_t)min(BY, NY - y0) * K * 2);
+        const uint32_t sb = lbase + (uint32_t)(it % NS) * SLOT;
 #pragma unroll
-        for (int i = 0; i < PW; ++i) issue_piece(st, i);
-        issue_end();
+        for (int i = 0; i < PW; ++i) {
+            int pi = w + NW * i;
+            if (pi >= P) pi -= NW;  // uneven piece count: a duplicate (same bytes, same place)
+            const bool isx = pi < PX;
+            const int prow = (isx ? pi : pi - PX) * RPP + lane / (BK / 8);
+            const int ch = nt_chunk<BK>(lane % (BK / 8), prow);
+            const uint32_t voff = (uint32_t)((prow * K + is_kt * BK + ch * 8) * 2), dst = sb + (uint32_t)pi * 1024u;
+            if constexpr (OPT & 8) {
+                if (isx) dma16(rx, voff, dst);
+                else dma16_nt(ry, voff, dst);
+            } else {
+                dma16(isx ? rx : ry, voff, dst);
+            }
+        }
+        if (++is_kt == nk) is_kt = 0, ++is_tile;
     };
 
     for (int d = 0; d < D && d < total; ++d) issue(d);
@@ -366,13 +348,8 @@ __global__ __launch_bounds__(64 * WX * WY) __attribute__((amdgpu_waves_per_eu((O
                     // epilogue stores of a tile that ended at step it - 1
                     vm_wait_rt(last_epi == it - 1 ? NST : 0);
                     lds_barrier();
-                    if constexpr (!(OPT & 8192)) {
-                        if (it + 2 < total) issue(it + 2);
-                    }
+                    if (it + 2 < total) issue(it + 2);
                     frags(it + 1, 0, ca, cb);
-                    if constexpr ((OPT & 8192) != 0) {  // the DMA issue behind the fragment reads
-                        if (it + 2 < total) issue(it + 2);
-                    }
                 }
                 if constexpr (OPT & 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -416,13 +393,8 @@ __global__ __launch_bounds__(64 * WX * WY) __attribute__((amdgpu_waves_per_eu((O
             const int ahead = min(D - 1, total - 1 - it);
             vm_wait_rt(ahead * PW + (it - last_epi <= D ? NST : 0));
             lds_barrier();
-            if constexpr (!(OPT & (48 | 128))) {
+            if constexpr (!(OPT & 48)) {
                 if (it + D < total) issue(it + D);
-            }
-            const bool do_issue = it + D < total;
-            IssueState ist{};  // OPT & 128: step it + D, its pieces issued one per MPP MFMAs
-            if constexpr ((OPT & 128) != 0) {
-                if (do_issue) ist = issue_begin(it + D);
             }
             const char* sx = lds + (it % NS) * SLOT;
             const char* sy = sx + BX * BK * 2;
@@ -444,32 +416,14 @@ __global__ __launch_bounds__(64 * WX * WY) __attribute__((amdgpu_waves_per_eu((O
                     if (s == 0 && it + D < total) issue(it + D);
                 }
                 if constexpr (OPT & 1) __builtin_amdgcn_s_setprio(1);
-                constexpr int MPP = (FX * FY * (BK / 32)) / PW > 0 ? (FX * FY * (BK / 32)) / PW : 1;
 #pragma unroll
                 for (int f = 0; f < FX; ++f)
 #pragma unroll
-                    for (int g = 0; g < FY; ++g) {
+                    for (int g = 0; g < FY; ++g)
                         acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[f], fb[g], acc[f][g], 0, 0, 0);
-                        if constexpr ((OPT & 128) != 0) {  // the next step's pieces between the MFMAs
-                            const int idx = s * FX * FY + f * FY + g;
-                            if ((idx % MPP) == MPP - 1 && idx / MPP < PW && do_issue) {
-                                __builtin_amdgcn_sched_barrier(0);
-                                issue_piece(ist, idx / MPP);
-                                __builtin_amdgcn_sched_barrier(0);
-                            }
-                        }
-                    }
                 if constexpr (OPT & 1) __builtin_amdgcn_s_setprio(0);
                 if constexpr ((OPT & 32) != 0) {
                     if (s == 0 && it + D < total) issue(it + D);
-                }
-            }
-            if constexpr ((OPT & 128) != 0) {
-                if (do_issue) {
-                    constexpr int MPP = (FX * FY * (BK / 32)) / PW > 0 ? (FX * FY * (BK / 32)) / PW : 1;
-#pragma unroll
-                    for (int i = (FX * FY * (BK / 32)) / MPP; i < PW; ++i) issue_piece(ist, i);
-                    issue_end();
                 }
             }
         }
@@ -487,145 +441,6 @@ __global__ __launch_bounds__(64 * WX * WY) __attribute__((amdgpu_waves_per_eu((O
                 Epi::template single<AUX>(ot, lb, xw + (FX - 1) * 16, yb + g * 16, G, acc[FX - 1][g]);
         }
         last_epi = it - 1;
-    }
-}
-
-// ---------------------------------------------------------------- NT kernel, loader waves
-// The same GEMM as fc_nt_kernel with the roles split between the waves: NC = WX*WY compute
-// waves (one per SIMD for NC = 4) only read fragments and issue MFMAs; NL loader waves (one
-// per SIMD beside them) only issue the LDS-DMA and wait for it. An LDS-DMA piece blocks its
-// issuing wave for ~60-180 cycles (MI355X_MICROARCH.md constants table); here that blocks a
-// loader wave, never the matrix stream. The ring has NS = 3 slots of BK = 64 k; one barrier per
-// step, placed between the step's two k-halves: the compute waves read step it's second half
-// into registers before its first-half MFMAs, so at barrier(it) slot it % 3 is fully consumed
-// and step it + 1 has landed (the loaders waited for it before arriving); after the barrier the
-// loaders issue step it + 3 into the freed slot and the compute waves read step it + 1's first
-// half while step it's second-half MFMAs (register operands) run. Loads run two steps ahead.
-// OPT: 1 = loaders at s_setprio 2, 2 = nontemporal output stores, 8 = nt Y-operand loads.
-template <int BX, int BY, int WX, int WY, int NL, int BK, int NS, class Epi, int OPT = 0>
-__global__ __launch_bounds__(64 * (WX * WY + NL)) __attribute__((amdgpu_waves_per_eu(2))) void fc_ws_kernel(
-    const __bf16* __restrict__ X, const __bf16* __restrict__ Y, int NY, int K, int ntx, int ntiles, Epi epi) {
-    constexpr int TX = BX / WX, TY = BY / WY, FX = TX / 16, FY = TY / 16;
-    constexpr int NC = WX * WY;
-    constexpr int RPP = 1024 / (BK * 2);
-    constexpr int PX = BX / RPP, P = (BX + BY) / RPP, PW = (P + NL - 1) / NL;  // pieces per loader
-    constexpr int SLOT = (BX + BY) * BK * 2;
-    constexpr int AUX = (OPT & 2) ? 2 : 0;
-    static_assert(BK == 64 && NS == 3 && FX * 16 == TX && FY * 16 == TY, "ws tile");
-    static_assert(BX % RPP == 0 && BY % RPP == 0 && 2 * PW < 64, "ws ring");
-    __shared__ __attribute__((aligned(16))) char lds[NS * SLOT + Epi::kLdsFloats * 4];
-    const int lane = threadIdx.x & 63, w = wave_id(), G = lane >> 4;
-    const int NG = gridDim.x, lg = xcd_remap(blockIdx.x, NG);
-    const int nk = K / BK;
-    const int total = ((ntiles - 1 - lg) / NG + 1) * nk;
-    const float* lb = (const float*)(lds + NS * SLOT);
-    epi.init((float*)(lds + NS * SLOT), threadIdx.x, 64 * (NC + NL));
-
-    if (w >= NC) {
-        // ---- loader waves
-        const int lw = w - NC;
-        const uint32_t lbase = lds_addr(lds);
-        int is_tile = 0, is_kt = 0;
-        auto issue = [&](int it) {
-            const int t = lg + is_tile * NG;
-            const int ty = t / ntx, tx = t - ty * ntx;
-            const int x0 = tx * BX, y0 = ty * BY;
-            const fi_i32x4 rx = make_rsrc(X + (size_t)x0 * K, (uint32_t)BX * K * 2);
-            const fi_i32x4 ry = make_rsrc(Y + (size_t)y0 * K, (uint32_t)min(BY, NY - y0) * K * 2);
-            const uint32_t sb = lbase + (uint32_t)(it % NS) * SLOT;
-#pragma unroll
-            for (int i = 0; i < PW; ++i) {
-                int pi = lw + NL * i;
-                if (pi >= P) pi -= NL;  // uneven piece count: a duplicate (same bytes, same place)
-                const bool isx = pi < PX;
-                const int prow = (isx ? pi : pi - PX) * RPP + lane / (BK / 8);
-                const int ch = nt_chunk<BK>(lane % (BK / 8), prow);
-                const uint32_t voff = (uint32_t)((prow * K + is_kt * BK + ch * 8) * 2), dst = sb + (uint32_t)pi * 1024u;
-                if constexpr (OPT & 8) {
-                    if (isx) dma16(rx, voff, dst);
-                    else dma16_nt(ry, voff, dst);
-                } else {
-                    dma16(isx ? rx : ry, voff, dst);
-                }
-            }
-            if (++is_kt == nk) is_kt = 0, ++is_tile;
-        };
-        if constexpr (OPT & 1) __builtin_amdgcn_s_setprio(2);
-        for (int d = 0; d < NS && d < total; ++d) issue(d);
-        if (total > 0) {
-            vm_wait_rt(min(NS - 1, total - 1) * PW);  // step 0 landed
-            lds_barrier();
-        }
-        for (int it = 0; it + 1 < total; ++it) {
-            // step it + 1 landed: younger are step it + 2's pieces (issued after barrier(it - 1))
-            vm_wait_rt(it + 2 < total ? PW : 0);
-            lds_barrier();  // barrier(it): slot it % 3 consumed by every compute wave
-            if (it + NS < total) issue(it + NS);
-        }
-        return;
-    }
-
-    // ---- compute waves
-    const int wx = w / WY, wy = w % WY;
-    auto frags = [&](int step, int s, bf16x8* fa, bf16x8* fb) {
-        const char* sx = lds + (step % NS) * SLOT;
-        const char* sy = sx + BX * BK * 2;
-        const int ch = s * 4 + G;
-#pragma unroll
-        for (int f = 0; f < FX; ++f) {
-            const int row = wx * TX + f * 16 + (lane & 15);
-            fa[f] = *(const bf16x8*)(sx + row * (BK * 2) + (nt_chunk<BK>(ch, row) << 4));
-        }
-#pragma unroll
-        for (int g = 0; g < FY; ++g) {
-            const int row = wy * TY + g * 16 + (lane & 15);
-            fb[g] = *(const bf16x8*)(sy + row * (BK * 2) + (nt_chunk<BK>(ch, row) << 4));
-        }
-    };
-    bf16x8 ca[FX], cb[FY];
-    if (total > 0) {
-        lds_barrier();  // step 0 landed (and the epilogue's LDS constants written)
-        frags(0, 0, ca, cb);
-    }
-    const int mytiles = total / nk;
-    int it = 0;
-    for (int tile_it = 0; tile_it < mytiles; ++tile_it) {
-        f32x4 acc[FX][FY];
-#pragma unroll
-        for (int f = 0; f < FX; ++f)
-#pragma unroll
-            for (int g = 0; g < FY; ++g) acc[f][g] = f32x4{0.f, 0.f, 0.f, 0.f};
-        for (int kt = 0; kt < nk; ++kt, ++it) {
-            bf16x8 ha[FX], hb[FY];
-            frags(it, 1, ha, hb);
-#pragma unroll
-            for (int f = 0; f < FX; ++f)
-#pragma unroll
-                for (int g = 0; g < FY; ++g)
-                    acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ca[f], cb[g], acc[f][g], 0, 0, 0);
-            if (it + 1 < total) {
-                lds_barrier();  // barrier(it)
-                frags(it + 1, 0, ca, cb);
-            }
-#pragma unroll
-            for (int f = 0; f < FX; ++f)
-#pragma unroll
-                for (int g = 0; g < FY; ++g)
-                    acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ha[f], hb[g], acc[f][g], 0, 0, 0);
-        }
-        const int t = lg + tile_it * NG;
-        const int ty = t / ntx, tx = t - ty * ntx;
-        const int y0 = ty * BY;
-        const OutTile ot = epi.tile(y0, min(BY, NY - y0));
-        const int xw = tx * BX + wx * TX, yb = y0 + wy * TY + (lane & 15);
-#pragma unroll
-        for (int g = 0; g < FY; ++g) {
-#pragma unroll
-            for (int f = 0; f + 1 < FX; f += 2)
-                Epi::template pair<AUX>(ot, lb, xw + f * 16, yb + g * 16, G, acc[f][g], acc[f + 1][g]);
-            if constexpr (FX % 2)
-                Epi::template single<AUX>(ot, lb, xw + (FX - 1) * 16, yb + g * 16, G, acc[FX - 1][g]);
-        }
     }
 }
 
@@ -737,9 +552,9 @@ __global__ __launch_bounds__(512) void fc_tn_kernel(const __bf16* __restrict__ X
 
 #ifndef FI_FC_CONFIG_OVERRIDE
 // (BX, BY, WX, WY, BK, NS[, OPT]) chosen with scripts/fc_bench.hip (interleaved A/B at R = 413,696)
-// forward: 256 output columns x 256 rows, waves 4 (x) x 2 (y), 2 slots of k 64, s_setprio, the
-// next step's DMA issued after the first fragment reads (round 4: 1.257 -> 1.225 ms)
-#define FC_FW_CFG 256, 256, 4, 2, 64, 2, 1 | 16
+// forward: 256 output columns x 256 rows, waves 4 (x) x 2 (y), 2 slots of k 64, one barrier per
+// step between its two halves, non-temporal frame loads (round 4: 1.257 -> 1.17-1.20 ms)
+#define FC_FW_CFG 256, 256, 4, 2, 64, 2, 8 | 4096
 // dgrad: 3136 = 14 x 224 output columns, 256 rows, waves 1 x 8 (14 x 2 fragments per wave),
 // s_setprio, non-temporal da3 stores (round 4: 1.652 -> 1.591 ms)
 #define FC_DG_CFG 224, 256, 1, 8, 64, 2, 1 | 2
@@ -753,7 +568,7 @@ template <int BX, int BY, int WX, int WY, int BK, int NS, int OPT = 0>
 static int fc_fwd_impl(const __bf16* a3, const __bf16* wT, const float* bias, __bf16* h, int rows, hipStream_t s) {
     FI_REQUIRE(rows > 0, "fc_fwd: rows must be positive");
     const int ntx = FCO / BX, nty = (rows + BY - 1) / BY, nt = ntx * nty;
-    hipLaunchKernelGGL((fc_nt_kernel<BX, BY, WX, WY, BK, NS, EpiFwd, OPT>), dim3(std::min(nt, (OPT & 256) ? 512 : 256)), dim3(64 * WX * WY), 0, s, wT, a3,
+    hipLaunchKernelGGL((fc_nt_kernel<BX, BY, WX, WY, BK, NS, EpiFwd, OPT>), dim3(std::min(nt, 256)), dim3(64 * WX * WY), 0, s, wT, a3,
                            rows, FCK, ntx, nt, EpiFwd{{h}, bias});
     FI_HIP_CHECK(hipGetLastError());
     return FI_OK;
@@ -763,28 +578,8 @@ template <int BX, int BY, int WX, int WY, int BK, int NS, int OPT = 0>
 static int fc_dgrad_impl(const __bf16* dh, const __bf16* w, __bf16* da3, int rows, hipStream_t s) {
     FI_REQUIRE(rows > 0, "fc_dgrad: rows must be positive");
     const int ntx = FCK / BX, nty = (rows + BY - 1) / BY, nt = ntx * nty;
-    hipLaunchKernelGGL((fc_nt_kernel<BX, BY, WX, WY, BK, NS, EpiDgrad, OPT>), dim3(std::min(nt, (OPT & 256) ? 512 : 256)), dim3(64 * WX * WY), 0, s, w,
+    hipLaunchKernelGGL((fc_nt_kernel<BX, BY, WX, WY, BK, NS, EpiDgrad, OPT>), dim3(std::min(nt, 256)), dim3(64 * WX * WY), 0, s, w,
                            dh, rows, FCO, ntx, nt, EpiDgrad{{da3}});
-    FI_HIP_CHECK(hipGetLastError());
-    return FI_OK;
-}
-
-template <int BX, int BY, int WX, int WY, int NL, int OPT = 0>
-static int fc_fwd_ws_impl(const __bf16* a3, const __bf16* wT, const float* bias, __bf16* h, int rows, hipStream_t s) {
-    FI_REQUIRE(rows > 0, "fc_fwd: rows must be positive");
-    const int ntx = FCO / BX, nty = (rows + BY - 1) / BY, nt = ntx * nty;
-    hipLaunchKernelGGL((fc_ws_kernel<BX, BY, WX, WY, NL, 64, 3, EpiFwd, OPT>), dim3(std::min(nt, 256)),
-                       dim3(64 * (WX * WY + NL)), 0, s, wT, a3, rows, FCK, ntx, nt, EpiFwd{{h}, bias});
-    FI_HIP_CHECK(hipGetLastError());
-    return FI_OK;
-}
-
-template <int BX, int BY, int WX, int WY, int NL, int OPT = 0>
-static int fc_dgrad_ws_impl(const __bf16* dh, const __bf16* w, __bf16* da3, int rows, hipStream_t s) {
-    FI_REQUIRE(rows > 0, "fc_dgrad: rows must be positive");
-    const int ntx = FCK / BX, nty = (rows + BY - 1) / BY, nt = ntx * nty;
-    hipLaunchKernelGGL((fc_ws_kernel<BX, BY, WX, WY, NL, 64, 3, EpiDgrad, OPT>), dim3(std::min(nt, 256)),
-                       dim3(64 * (WX * WY + NL)), 0, s, w, dh, rows, FCO, ntx, nt, EpiDgrad{{da3}});
     FI_HIP_CHECK(hipGetLastError());
     return FI_OK;
 }

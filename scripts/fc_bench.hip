@@ -4,11 +4,12 @@
 // GEMM (same k order per output element, so the results must be identical).
 // Build: scripts/build_fc_bench.sh; run: build/fc_bench [rounds]
 #define FI_FC_CONFIG_OVERRIDE
-#define FC_FW_CFG 256, 256, 4, 2, 64, 2, 1 | 16
+#define FC_FW_CFG 256, 256, 4, 2, 64, 2, 8 | 4096
 #define FC_DG_CFG 224, 256, 1, 8, 64, 2, 1 | 2
 #define FC_WG_CFG 256, 224, 4, 2, 64, 2
 #include "../freeimpala_amd/csrc/fc_gemm.hip"
 #include "../freeimpala_amd/csrc/fc_blaslt.h"
+#include "fc_variants.hip"
 
 #include <cstdio>
 #include <algorithm>
@@ -79,16 +80,10 @@ int main(int argc, char** argv) {
 #define DGSV(nm, ...) add("dgrd " nm, 1, [&](hipStream_t st, int k) { return fc_dgrad_ws_impl<__VA_ARGS__>(dh, w, da3[k], R, st); }, da3[0], da3[1], (size_t)R * FCK * 2)
 #define WGV(nm, S, ...) add("wgrd " nm, 2, [&](hipStream_t st, int k) { return fc_wgrad_impl<__VA_ARGS__>(a3, dh, slab, dw[k], R, st, S); }, dw[0], dw[1], (size_t)FCK * FCO * 4)
     // the shipped configurations first (fc_gemm.hip FC_*_CFG), then alternatives
-    FWDV("256x256 w4x2 bk64 ns2 prio iss@frag", 256, 256, 4, 2, 64, 2, 1 | 16);
     FWDV("256x256 w4x2 bk64 ns2 ntY midbar", 256, 256, 4, 2, 64, 2, 8 | 4096);
-    FWSV("ws 256x128 c2x2 l4", 256, 128, 2, 2, 4, 0);
-    FWSV("ws 256x128 c2x2 l4 lprio", 256, 128, 2, 2, 4, 1);
+    FWDV("256x256 w4x2 bk64 ns2 prio iss@frag", 256, 256, 4, 2, 64, 2, 1 | 16);
     FWSV("ws 256x128 c2x2 l4 ntY", 256, 128, 2, 2, 4, 8);
-    FWSV("ws 128x256 c2x2 l4", 128, 256, 2, 2, 4, 0);
-    FWSV("ws 256x128 c2x2 l2", 256, 128, 2, 2, 2, 0);
     DGV("224x256 w1x8 bk64 ns2 prio ntst", 224, 256, 1, 8, 64, 2, 1 | 2);
-    DGSV("ws 224x128 c2x2 l4 ntst", 224, 128, 2, 2, 4, 2);
-    DGSV("ws 224x128 c1x4 l4 ntst", 224, 128, 1, 4, 4, 2);
     DGSV("ws 224x128 c2x2 l4 ntst lprio", 224, 128, 2, 2, 4, 3);
     WGV("256x224 w4x2 bk64 ns2", 9, 256, 224, 4, 2, 64, 2);
     // hipBLASLt (the default fwd / dgrad today), own output buffers: not bit-comparable

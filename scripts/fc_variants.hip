@@ -1,0 +1,172 @@
+// fc_variants.hip -- bench-only fc GEMM variants measured against the shipped kernels in
+// scripts/fc_bench.hip (included after freeimpala_amd/csrc/fc_gemm.hip; not part of the library).
+// Round 4: the loader-wave NT kernel below measured 1.16 ms forward / 1.62-1.66 ms dgrad against
+// 1.17-1.21 / 1.60 for the shipped 8-wave kernels and 0.99 / 1.35 for hipBLASLt
+// (profiles/r04_fc_bench_variants.txt), so it stays here.
+namespace fi {
+namespace fcg {
+
+// ---------------------------------------------------------------- NT kernel, loader waves
+// The same GEMM as fc_nt_kernel with the roles split between the waves: NC = WX*WY compute
+// waves (one per SIMD for NC = 4) only read fragments and issue MFMAs; NL loader waves (one
+// per SIMD beside them) only issue the LDS-DMA and wait for it. An LDS-DMA piece blocks its
+// issuing wave for ~60-180 cycles (MI355X_MICROARCH.md constants table); here that blocks a
+// loader wave, never the matrix stream. The ring has NS = 3 slots of BK = 64 k; one barrier per
+// step, placed between the step's two k-halves: the compute waves read step it's second half
+// into registers before its first-half MFMAs, so at barrier(it) slot it % 3 is fully consumed
+// and step it + 1 has landed (the loaders waited for it before arriving); after the barrier the
+// loaders issue step it + 3 into the freed slot and the compute waves read step it + 1's first
+// half while step it's second-half MFMAs (register operands) run. Loads run two steps ahead.
+// OPT: 1 = loaders at s_setprio 2, 2 = nontemporal output stores, 8 = nt Y-operand loads.
+template <int BX, int BY, int WX, int WY, int NL, int BK, int NS, class Epi, int OPT = 0>
+__global__ __launch_bounds__(64 * (WX * WY + NL)) __attribute__((amdgpu_waves_per_eu(2))) void fc_ws_kernel(
+    const __bf16* __restrict__ X, const __bf16* __restrict__ Y, int NY, int K, int ntx, int ntiles, Epi epi) {
+    constexpr int TX = BX / WX, TY = BY / WY, FX = TX / 16, FY = TY / 16;
+    constexpr int NC = WX * WY;
+    constexpr int RPP = 1024 / (BK * 2);
+    constexpr int PX = BX / RPP, P = (BX + BY) / RPP, PW = (P + NL - 1) / NL;  // pieces per loader
+    constexpr int SLOT = (BX + BY) * BK * 2;
+    constexpr int AUX = (OPT & 2) ? 2 : 0;
+    static_assert(BK == 64 && NS == 3 && FX * 16 == TX && FY * 16 == TY, "ws tile");
+    static_assert(BX % RPP == 0 && BY % RPP == 0 && 2 * PW < 64, "ws ring");
+    __shared__ __attribute__((aligned(16))) char lds[NS * SLOT + Epi::kLdsFloats * 4];
+    const int lane = threadIdx.x & 63, w = wave_id(), G = lane >> 4;
+    const int NG = gridDim.x, lg = xcd_remap(blockIdx.x, NG);
+    const int nk = K / BK;
+    const int total = ((ntiles - 1 - lg) / NG + 1) * nk;
+    const float* lb = (const float*)(lds + NS * SLOT);
+    epi.init((float*)(lds + NS * SLOT), threadIdx.x, 64 * (NC + NL));
+
+    if (w >= NC) {
+        // ---- loader waves
+        const int lw = w - NC;
+        const uint32_t lbase = lds_addr(lds);
+        int is_tile = 0, is_kt = 0;
+        auto issue = [&](int it) {
+            const int t = lg + is_tile * NG;
+            const int ty = t / ntx, tx = t - ty * ntx;
+            const int x0 = tx * BX, y0 = ty * BY;
+            const fi_i32x4 rx = make_rsrc(X + (size_t)x0 * K, (uint32_t)BX * K * 2);
+            const fi_i32x4 ry = make_rsrc(Y + (size_t)y0 * K, (uint32_t)min(BY, NY - y0) * K * 2);
+            const uint32_t sb = lbase + (uint32_t)(it % NS) * SLOT;
+#pragma unroll
+            for (int i = 0; i < PW; ++i) {
+                int pi = lw + NL * i;
+                if (pi >= P) pi -= NL;  // uneven piece count: a duplicate (same bytes, same place)
+                const bool isx = pi < PX;
+                const int prow = (isx ? pi : pi - PX) * RPP + lane / (BK / 8);
+                const int ch = nt_chunk<BK>(lane % (BK / 8), prow);
+                const uint32_t voff = (uint32_t)((prow * K + is_kt * BK + ch * 8) * 2), dst = sb + (uint32_t)pi * 1024u;
+                if constexpr (OPT & 8) {
+                    if (isx) dma16(rx, voff, dst);
+                    else dma16_nt(ry, voff, dst);
+                } else {
+                    dma16(isx ? rx : ry, voff, dst);
+                }
+            }
+            if (++is_kt == nk) is_kt = 0, ++is_tile;
+        };
+        if constexpr (OPT & 1) __builtin_amdgcn_s_setprio(2);
+        for (int d = 0; d < NS && d < total; ++d) issue(d);
+        if (total > 0) {
+            vm_wait_rt(min(NS - 1, total - 1) * PW);  // step 0 landed
+            lds_barrier();
+        }
+        for (int it = 0; it + 1 < total; ++it) {
+            // step it + 1 landed: younger are step it + 2's pieces (issued after barrier(it - 1))
+            vm_wait_rt(it + 2 < total ? PW : 0);
+            lds_barrier();  // barrier(it): slot it % 3 consumed by every compute wave
+            if (it + NS < total) issue(it + NS);
+        }
+        return;
+    }
+
+    // ---- compute waves
+    const int wx = w / WY, wy = w % WY;
+    auto frags = [&](int step, int s, bf16x8* fa, bf16x8* fb) {
+        const char* sx = lds + (step % NS) * SLOT;
+        const char* sy = sx + BX * BK * 2;
+        const int ch = s * 4 + G;
+#pragma unroll
+        for (int f = 0; f < FX; ++f) {
+            const int row = wx * TX + f * 16 + (lane & 15);
+            fa[f] = *(const bf16x8*)(sx + row * (BK * 2) + (nt_chunk<BK>(ch, row) << 4));
+        }
+#pragma unroll
+        for (int g = 0; g < FY; ++g) {
+            const int row = wy * TY + g * 16 + (lane & 15);
+            fb[g] = *(const bf16x8*)(sy + row * (BK * 2) + (nt_chunk<BK>(ch, row) << 4));
+        }
+    };
+    bf16x8 ca[FX], cb[FY];
+    if (total > 0) {
+        lds_barrier();  // step 0 landed (and the epilogue's LDS constants written)
+        frags(0, 0, ca, cb);
+    }
+    const int mytiles = total / nk;
+    int it = 0;
+    for (int tile_it = 0; tile_it < mytiles; ++tile_it) {
+        f32x4 acc[FX][FY];
+#pragma unroll
+        for (int f = 0; f < FX; ++f)
+#pragma unroll
+            for (int g = 0; g < FY; ++g) acc[f][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int kt = 0; kt < nk; ++kt, ++it) {
+            bf16x8 ha[FX], hb[FY];
+            frags(it, 1, ha, hb);
+#pragma unroll
+            for (int f = 0; f < FX; ++f)
+#pragma unroll
+                for (int g = 0; g < FY; ++g)
+                    acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ca[f], cb[g], acc[f][g], 0, 0, 0);
+            if (it + 1 < total) {
+                lds_barrier();  // barrier(it)
+                frags(it + 1, 0, ca, cb);
+            }
+#pragma unroll
+            for (int f = 0; f < FX; ++f)
+#pragma unroll
+                for (int g = 0; g < FY; ++g)
+                    acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ha[f], hb[g], acc[f][g], 0, 0, 0);
+        }
+        const int t = lg + tile_it * NG;
+        const int ty = t / ntx, tx = t - ty * ntx;
+        const int y0 = ty * BY;
+        const OutTile ot = epi.tile(y0, min(BY, NY - y0));
+        const int xw = tx * BX + wx * TX, yb = y0 + wy * TY + (lane & 15);
+#pragma unroll
+        for (int g = 0; g < FY; ++g) {
+#pragma unroll
+            for (int f = 0; f + 1 < FX; f += 2)
+                Epi::template pair<AUX>(ot, lb, xw + f * 16, yb + g * 16, G, acc[f][g], acc[f + 1][g]);
+            if constexpr (FX % 2)
+                Epi::template single<AUX>(ot, lb, xw + (FX - 1) * 16, yb + g * 16, G, acc[FX - 1][g]);
+        }
+    }
+}
+
+}  // namespace fcg
+
+using namespace fcg;
+
+template <int BX, int BY, int WX, int WY, int NL, int OPT = 0>
+static int fc_fwd_ws_impl(const __bf16* a3, const __bf16* wT, const float* bias, __bf16* h, int rows, hipStream_t s) {
+    FI_REQUIRE(rows > 0, "fc_fwd: rows must be positive");
+    const int ntx = FCO / BX, nty = (rows + BY - 1) / BY, nt = ntx * nty;
+    hipLaunchKernelGGL((fc_ws_kernel<BX, BY, WX, WY, NL, 64, 3, EpiFwd, OPT>), dim3(std::min(nt, 256)),
+                       dim3(64 * (WX * WY + NL)), 0, s, wT, a3, rows, FCK, ntx, nt, EpiFwd{{h}, bias});
+    FI_HIP_CHECK(hipGetLastError());
+    return FI_OK;
+}
+
+template <int BX, int BY, int WX, int WY, int NL, int OPT = 0>
+static int fc_dgrad_ws_impl(const __bf16* dh, const __bf16* w, __bf16* da3, int rows, hipStream_t s) {
+    FI_REQUIRE(rows > 0, "fc_dgrad: rows must be positive");
+    const int ntx = FCK / BX, nty = (rows + BY - 1) / BY, nt = ntx * nty;
+    hipLaunchKernelGGL((fc_ws_kernel<BX, BY, WX, WY, NL, 64, 3, EpiDgrad, OPT>), dim3(std::min(nt, 256)),
+                       dim3(64 * (WX * WY + NL)), 0, s, w, dh, rows, FCO, ntx, nt, EpiDgrad{{da3}});
+    FI_HIP_CHECK(hipGetLastError());
+    return FI_OK;
+}
+
+}  // namespace fi
