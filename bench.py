@@ -10,8 +10,10 @@ trajectories already resident in HBM. value = T * B_per_gpu * N * K / max-over-r
 
 The roofline object is measured live: HIP events around every kernel launch of a few
 profiled steps (after the timed region) give each kernel's mean duration; ALGORITHMIC work
-per launch / duration vs the MI355X peak. cpu_baseline times the C
-oracle (oracle/, kind "port") on rank 0 on a bounded sample of the same workload.
+per launch / duration vs the MI355X peak. cpu_baseline times the
+torch-CPU port of the step under oracle/ (kind "port") on rank 0: whole T x 4096 steps (the
+Atari step takes ~50 s on 16 cores and ~120 GB of host memory; with less headroom, or
+--cpu-sample, a bounded sample extrapolated to B=4096).
 """
 from __future__ import annotations
 
@@ -80,12 +82,41 @@ def host_cpu_info():
             "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
 
 
+def host_mem_headroom_gb():
+    """Host memory this process may still take: MemAvailable, capped by the cgroup's limit
+    (a gpurun box caps one command at ~270 GiB of a much larger host)."""
+    avail = None
+    try:
+        with open("/proc/meminfo") as fh:
+            for line in fh:
+                if line.startswith("MemAvailable:"):
+                    avail = int(line.split()[1]) * 1024
+    except OSError:
+        pass
+    try:
+        with open("/sys/fs/cgroup/memory.max") as fh:
+            lim = fh.read().strip()
+        with open("/sys/fs/cgroup/memory.current") as fh:
+            cur = int(fh.read().strip())
+        if lim != "max":
+            room = int(lim) - cur
+            avail = room if avail is None else min(avail, room)
+    except (OSError, ValueError):
+        pass
+    return None if avail is None else avail / 2**30
+
+
+CPU_FULL_GB = 200  # the whole B=4096 Atari CPU step peaks at ~118 GB RSS (measured on a pool box)
+
+
 def cpu_baseline(arch, T, A, seconds, threads, full=False):
     """Time a CPU learner step on rank 0 (test infrastructure under oracle/, kind 'port'):
     the torch-CPU port of the step (oracle/torch_learner.py: oneDNN/MKL fp32 convolutions and
     GEMMs, autograd, the same V-trace/loss/clip/Adam as the C oracle; gradient-equal to it,
-    tests/test_torch_baseline.py) on a bounded sample of the workload. The C oracle's own
-    V-trace + loss at the full T x 4096 is reported beside it."""
+    tests/test_torch_baseline.py). MLP: whole T x 4096 steps. Atari: one whole T x 4096 step
+    when `full` (bench.py's default when the host has the memory for it), else a bounded sample
+    extrapolated flat in B. The C oracle's own V-trace + loss at the full T x 4096 is reported
+    beside it."""
     import numpy as np
     import torch
     from oracle import oracle as orc
@@ -116,11 +147,13 @@ def cpu_baseline(arch, T, A, seconds, threads, full=False):
                   f"T={T}, full B=4096 (min of 2 steps, {per_b[4096]:.2f} s; B=512: {per_b[512]:.3f} s "
                   f"= {T * 512 / per_b[512]:.0f} env-steps/s)")
         extrap = False
-    elif full:  # --cpu-full: one whole T x 4096 step (~1 min, ~150 GB of host memory)
+    elif full:  # one whole T x 4096 step (~50 s on 16 cores, ~120 GB of host memory)
+        import resource
         Bs = 4096
         step = one(Bs)
+        rss = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20
         sample = (f"torch-CPU port of the Atari-net learner step (fwd+vtrace+bwd+clip+adam, fp32), "
-                  f"T={T}, the full B=4096 (one step, {step:.1f} s)")
+                  f"T={T}, the full B=4096 (one step, {step:.1f} s, peak RSS {rss:.0f} GB)")
         extrap = False
     else:
         t = one(2)
@@ -129,7 +162,8 @@ def cpu_baseline(arch, T, A, seconds, threads, full=False):
         step = min(one(Bs) for _ in range(2))
         sample = (f"torch-CPU port of the Atari-net learner step (fwd+vtrace+bwd+clip+adam, fp32), "
                   f"T={T}, B={Bs} per step (min of 2 steps, {step:.2f} s each); EXTRAPOLATED to "
-                  f"B=4096 as env-steps/s flat in B (a full B=4096 step: bench.py --cpu-full)")
+                  f"B=4096 as env-steps/s flat in B (the full B=4096 step needs {CPU_FULL_GB} GB of "
+                  f"host memory headroom; bench.py --cpu-full forces it)")
         extrap = Bs < 4096
     # V-trace + loss + grads alone at the full config size (the C oracle)
     case = orc.synth_batch(7, T=T, B=4096, A=A, D=1, obs=False)
@@ -160,7 +194,10 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-full", action="store_true",
-                    help="time one whole T x 4096 CPU step for cpu_baseline (Atari: ~1 min, ~150 GB host memory)")
+                    help="time one whole T x 4096 Atari CPU step for cpu_baseline whatever the memory headroom")
+    ap.add_argument("--cpu-sample", action="store_true",
+                    help="Atari cpu_baseline from a bounded sample extrapolated to B=4096 (the default is "
+                         f"one whole step when {CPU_FULL_GB} GB of host memory are free)")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
@@ -293,7 +330,13 @@ def main():
         # on the pool's boxes, whose nproc counts the whole host), else the affinity mask
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or host_cpu_info()["affinity_cpus"] or 1
         try:
-            result["cpu_baseline"] = cpu_baseline(args.arch, T, A, args.cpu_seconds, threads, full=args.cpu_full)
+            room = host_mem_headroom_gb()
+            full = args.cpu_full or (not args.cpu_sample and args.batch == 4096 and room is not None
+                                     and room >= CPU_FULL_GB)
+            result["cpu_baseline"] = cpu_baseline(args.arch, T, A, args.cpu_seconds, threads, full=full)
+            if args.arch == "atari" and not full:
+                result["cpu_baseline"]["full_step_skipped"] = (
+                    "--cpu-sample" if args.cpu_sample else f"host memory headroom {room and round(room, 1)} GB < {CPU_FULL_GB} GB")
             result["cpu_baseline"]["threads_basis"] = (
                 "OMP_NUM_THREADS from the environment: the pool gives one GPU's job a 16-CPU share and "
                 "sets OMP_NUM_THREADS=16 (nproc / the affinity mask count the whole host, shared with "
