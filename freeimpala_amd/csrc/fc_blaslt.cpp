@@ -215,7 +215,8 @@ FcBlasLt* fc_blaslt_create(int rows, const void* a3, const void* w, const void* 
         rc = FI_ERR_OOM;
     }
     constexpr int K = 3136, N = 512;
-    if (rc == FI_OK) {  // timing data (every buffer is overwritten by the step before it is read)
+    if (rc == FI_OK) {  // timing data: the step overwrites a3 / h / da3 before reading them, and dh rows
+        // T*B..N (never written by the step) get their zeros from atari_create, which runs after this call
         rc = fill_hash_bf16((void*)a3, (size_t)rows * K, 1u, s);
         if (rc == FI_OK) rc = fill_hash_bf16((void*)dh, (size_t)rows * N, 2u, s);
         if (rc == FI_OK) rc = fill_hash_bf16((void*)w, (size_t)K * N, 3u, s);
