@@ -109,6 +109,23 @@ def host_mem_headroom_gb():
 CPU_FULL_GB = 200  # the whole B=4096 Atari CPU step peaks at ~118 GB RSS (measured on a pool box)
 
 
+def full_cpu_step(arch, batch, cpu_full, cpu_sample, room_gb):
+    """(run one whole T x 4096 Atari CPU step?, why not). --cpu-full forces it; otherwise it
+    runs at the metric's B = 4096 when the host has CPU_FULL_GB of headroom, unless
+    --cpu-sample asks for the bounded, extrapolated sample. MLP steps always run whole."""
+    if arch != "atari":
+        return False, None
+    if cpu_full:
+        return True, None
+    if cpu_sample:
+        return False, "--cpu-sample"
+    if batch != 4096:
+        return False, f"B={batch}: the full step is timed at the metric's B=4096 only"
+    if room_gb is None or room_gb < CPU_FULL_GB:
+        return False, f"host memory headroom {room_gb and round(room_gb, 1)} GB < {CPU_FULL_GB} GB"
+    return True, None
+
+
 def cpu_baseline(arch, T, A, seconds, threads, full=False):
     """Time a CPU learner step on rank 0 (test infrastructure under oracle/, kind 'port'):
     the torch-CPU port of the step (oracle/torch_learner.py: oneDNN/MKL fp32 convolutions and
@@ -330,13 +347,11 @@ def main():
         # on the pool's boxes, whose nproc counts the whole host), else the affinity mask
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or host_cpu_info()["affinity_cpus"] or 1
         try:
-            room = host_mem_headroom_gb()
-            full = args.cpu_full or (not args.cpu_sample and args.batch == 4096 and room is not None
-                                     and room >= CPU_FULL_GB)
+            full, why_not = full_cpu_step(args.arch, args.batch, args.cpu_full, args.cpu_sample,
+                                          host_mem_headroom_gb())
             result["cpu_baseline"] = cpu_baseline(args.arch, T, A, args.cpu_seconds, threads, full=full)
-            if args.arch == "atari" and not full:
-                result["cpu_baseline"]["full_step_skipped"] = (
-                    "--cpu-sample" if args.cpu_sample else f"host memory headroom {room and round(room, 1)} GB < {CPU_FULL_GB} GB")
+            if why_not:
+                result["cpu_baseline"]["full_step_skipped"] = why_not
             result["cpu_baseline"]["threads_basis"] = (
                 "OMP_NUM_THREADS from the environment: the pool gives one GPU's job a 16-CPU share and "
                 "sets OMP_NUM_THREADS=16 (nproc / the affinity mask count the whole host, shared with "
