@@ -481,8 +481,22 @@ __global__ __launch_bounds__(512) void fc_tn_kernel(const __bf16* __restrict__ X
     const int lane = threadIdx.x & 63, w = wave_id();
     const int wx = w / WY, wy = w % WY;
     const int ntx = NXT / BX, nty = NYT / BY;
-    const int lg = xcd_remap(blockIdx.x, gridDim.x);
-    const int sp = lg / (ntx * nty), rem = lg - sp * (ntx * nty);
+    // workgroup -> (R-slice, tile). Block b runs on XCD b % 8 (round-robin dispatch): whole
+    // slices first, S / 8 of them per XCD, so the NT tiles of a slice share one XCD's L2 and the
+    // slice's rows leave HBM once (with the slices laid contiguously over the XCDs, 9 slices on 8
+    // XCDs straddled them: 1.47x the algorithmic traffic); the tiles of the S % 8 leftover slices
+    // follow (XCD-contiguous when there is no whole slice per XCD, i.e. small R)
+    const int NT = ntx * nty, per = (int)(gridDim.x / NT) / 8;
+    const int b = blockIdx.x, j = b / 8;
+    int sp, rem;
+    if (j < per * NT) {
+        sp = (b % 8) * per + j / NT;
+        rem = j - (j / NT) * NT;
+    } else {
+        const int id = per > 0 ? b - 8 * per * NT : xcd_remap(b, gridDim.x);
+        sp = 8 * per + id / NT;
+        rem = id - (id / NT) * NT;
+    }
     const int tx = rem / nty, ty = rem - tx * nty;
     const int x0 = tx * BX, y0 = ty * BY;
     const int rbeg = sp * rps, rend = min(R, rbeg + rps);
