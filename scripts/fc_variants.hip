@@ -145,6 +145,131 @@ __global__ __launch_bounds__(64 * (WX * WY + NL)) __attribute__((amdgpu_waves_pe
     }
 }
 
+
+// ---------------------------------------------------------------- forward, one DMA block per step
+// fc_nt_kernel<256, 256, 4, 2, 64, 2, Epi, 8 | 4096> (the shipped forward) with the step's 8 LDS-DMA
+// pieces per wave issued from ONE asm block the way hipBLASLt's loop issues them: per-lane offsets
+// computed once (constant across steps), the k advance in the instruction's soffset SGPR, M0
+// advanced by one s_add per piece, one s_nop for the descriptor hazard per step instead of per piece.
+#define FI_FC2_LOADS(NTY)                                                                         \
+    "s_nop 4\n\ts_mov_b32 %[keep], m0\n\ts_mov_b32 m0, %[mx]\n\ts_nop 0\n\t"                      \
+    "buffer_load_dwordx4 %[v0], %[rx], %[ko] offen lds\n\ts_add_u32 m0, m0, 8192\n\t"            \
+    "buffer_load_dwordx4 %[v1], %[rx], %[ko] offen lds\n\ts_add_u32 m0, m0, 8192\n\t"            \
+    "buffer_load_dwordx4 %[v2], %[rx], %[ko] offen lds\n\ts_add_u32 m0, m0, 8192\n\t"            \
+    "buffer_load_dwordx4 %[v3], %[rx], %[ko] offen lds\n\ts_mov_b32 m0, %[my]\n\ts_nop 0\n\t"    \
+    "buffer_load_dwordx4 %[v4], %[ry], %[ko] offen " NTY " lds\n\ts_add_u32 m0, m0, 8192\n\t"    \
+    "buffer_load_dwordx4 %[v5], %[ry], %[ko] offen " NTY " lds\n\ts_add_u32 m0, m0, 8192\n\t"    \
+    "buffer_load_dwordx4 %[v6], %[ry], %[ko] offen " NTY " lds\n\ts_add_u32 m0, m0, 8192\n\t"    \
+    "buffer_load_dwordx4 %[v7], %[ry], %[ko] offen " NTY " lds\n\ts_mov_b32 m0, %[keep]"
+
+template <class Epi>
+__global__ __launch_bounds__(512) void fc_nt2_kernel(const __bf16* __restrict__ X, const __bf16* __restrict__ Y,
+                                                     int NY, int K, int ntx, int ntiles, Epi epi) {
+    constexpr int BX = 256, BY = 256, WX = 4, WY = 2, BK = 64, NS = 2;
+    constexpr int TX = BX / WX, TY = BY / WY, FX = TX / 16, FY = TY / 16;
+    constexpr int RPP = 1024 / (BK * 2), NW = WX * WY, PX = BX / RPP, PW = (BX + BY) / RPP / NW;
+    constexpr int SLOT = (BX + BY) * BK * 2;
+    constexpr int NST = FY * (FX / 2 + FX % 2);
+    static_assert(PW == 8 && PX == 4 * NW, "4 X pieces then 4 Y pieces per wave");
+    __shared__ __attribute__((aligned(16))) char lds[NS * SLOT + Epi::kLdsFloats * 4];
+    const int lane = threadIdx.x & 63, w = wave_id(), G = lane >> 4;
+    const int wx = w / WY, wy = w % WY;
+    const int NG = gridDim.x, lg = xcd_remap(blockIdx.x, NG);
+    const int nk = K / BK;
+    const int total = ((ntiles - 1 - lg) / NG + 1) * nk;
+    const uint32_t lbase = lds_addr(lds);
+    const float* lb = (const float*)(lds + NS * SLOT);
+    epi.init((float*)(lds + NS * SLOT), threadIdx.x, 64 * NW);
+    uint32_t vo[PW];  // piece i: X rows (w + 8i) * 8 + lane / 8 for i < 4, Y rows (w + 8(i - 4)) * 8 + ...
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+        const int prow = (w + NW * (i & 3)) * RPP + lane / (BK / 8);
+        vo[i] = (uint32_t)((prow * K + nt_chunk<BK>(lane % (BK / 8), prow) * 8) * 2);
+    }
+    int is_tile = 0, is_kt = 0;
+    auto issue = [&](int it) {
+        const int t = lg + is_tile * NG;
+        const int ty = t / ntx, tx = t - ty * ntx;
+        const fi_i32x4 rx = make_rsrc(X + (size_t)tx * BX * K, (uint32_t)BX * K * 2);
+        const fi_i32x4 ry = make_rsrc(Y + (size_t)ty * BY * K, (uint32_t)min(BY, NY - ty * BY) * K * 2);
+        const uint32_t mx = lbase + (uint32_t)(it % NS) * SLOT + (uint32_t)w * 1024u;
+        const uint32_t my = mx + (uint32_t)PX * 1024u, ko = (uint32_t)(is_kt * BK * 2);
+        uint32_t keep;
+        asm volatile(FI_FC2_LOADS("nt")
+                     : [keep] "=&s"(keep)
+                     : [v0] "v"(vo[0]), [v1] "v"(vo[1]), [v2] "v"(vo[2]), [v3] "v"(vo[3]), [v4] "v"(vo[4]),
+                       [v5] "v"(vo[5]), [v6] "v"(vo[6]), [v7] "v"(vo[7]), [rx] "s"(rx), [ry] "s"(ry), [ko] "s"(ko),
+                       [mx] "s"(mx), [my] "s"(my)
+                     : "memory");
+        if (++is_kt == nk) is_kt = 0, ++is_tile;
+    };
+    auto frags = [&](int step, int s, bf16x8* fa, bf16x8* fb) {
+        const char* sx = lds + (step % NS) * SLOT;
+        const char* sy = sx + BX * BK * 2;
+        const int ch = s * 4 + G;
+#pragma unroll
+        for (int f = 0; f < FX; ++f) {
+            const int row = wx * TX + f * 16 + (lane & 15);
+            fa[f] = *(const bf16x8*)(sx + row * (BK * 2) + (nt_chunk<BK>(ch, row) << 4));
+        }
+#pragma unroll
+        for (int g = 0; g < FY; ++g) {
+            const int row = wy * TY + g * 16 + (lane & 15);
+            fb[g] = *(const bf16x8*)(sy + row * (BK * 2) + (nt_chunk<BK>(ch, row) << 4));
+        }
+    };
+    if (total > 0) issue(0);
+    bf16x8 ca[FX], cb[FY];
+    if (total > 0) {
+        vm_wait_rt(0);
+        lds_barrier();
+        if (1 < total) issue(1);
+        frags(0, 0, ca, cb);
+    }
+    const int mytiles = total / nk;
+    int it = 0, last_epi = -(1 << 20);
+    for (int tile_it = 0; tile_it < mytiles; ++tile_it) {
+        f32x4 acc[FX][FY];
+#pragma unroll
+        for (int f = 0; f < FX; ++f)
+#pragma unroll
+            for (int g = 0; g < FY; ++g) acc[f][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int kt = 0; kt < nk; ++kt, ++it) {
+            bf16x8 ha[FX], hb[FY];
+            frags(it, 1, ha, hb);
+#pragma unroll
+            for (int f = 0; f < FX; ++f)
+#pragma unroll
+                for (int g = 0; g < FY; ++g)
+                    acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ca[f], cb[g], acc[f][g], 0, 0, 0);
+            if (it + 1 < total) {
+                vm_wait_rt(last_epi == it - 1 ? NST : 0);
+                lds_barrier();
+                if (it + 2 < total) issue(it + 2);
+                frags(it + 1, 0, ca, cb);
+            }
+#pragma unroll
+            for (int f = 0; f < FX; ++f)
+#pragma unroll
+                for (int g = 0; g < FY; ++g)
+                    acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ha[f], hb[g], acc[f][g], 0, 0, 0);
+        }
+        const int t = lg + tile_it * NG;
+        const int ty = t / ntx, tx = t - ty * ntx;
+        const int y0 = ty * BY;
+        const OutTile ot = epi.tile(y0, min(BY, NY - y0));
+        const int xw = tx * BX + wx * TX, yb = y0 + wy * TY + (lane & 15);
+#pragma unroll
+        for (int g = 0; g < FY; ++g) {
+#pragma unroll
+            for (int f = 0; f + 1 < FX; f += 2)
+                Epi::template pair<0>(ot, lb, xw + f * 16, yb + g * 16, G, acc[f][g], acc[f + 1][g]);
+        }
+        last_epi = it - 1;
+    }
+}
+#undef FI_FC2_LOADS
+
 }  // namespace fcg
 
 using namespace fcg;
@@ -165,6 +290,15 @@ static int fc_dgrad_ws_impl(const __bf16* dh, const __bf16* w, __bf16* da3, int 
     const int ntx = FCK / BX, nty = (rows + BY - 1) / BY, nt = ntx * nty;
     hipLaunchKernelGGL((fc_ws_kernel<BX, BY, WX, WY, NL, 64, 3, EpiDgrad, OPT>), dim3(std::min(nt, 256)),
                        dim3(64 * (WX * WY + NL)), 0, s, w, dh, rows, FCO, ntx, nt, EpiDgrad{{da3}});
+    FI_HIP_CHECK(hipGetLastError());
+    return FI_OK;
+}
+
+static int fc_fwd2_impl(const __bf16* a3, const __bf16* wT, const float* bias, __bf16* h, int rows, hipStream_t s) {
+    FI_REQUIRE(rows > 0, "fc_fwd: rows must be positive");
+    const int ntx = FCO / 256, nty = (rows + 255) / 256, nt = ntx * nty;
+    hipLaunchKernelGGL((fc_nt2_kernel<EpiFwd>), dim3(std::min(nt, 256)), dim3(512), 0, s, wT, a3, rows, FCK, ntx, nt,
+                       EpiFwd{{h}, bias});
     FI_HIP_CHECK(hipGetLastError());
     return FI_OK;
 }
