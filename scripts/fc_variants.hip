@@ -1,3 +1,4 @@
+#include <tuple>
 // fc_variants.hip -- bench-only fc GEMM variants measured against the shipped kernels in
 // scripts/fc_bench.hip (included after freeimpala_amd/csrc/fc_gemm.hip; not part of the library).
 // Round 4: the loader-wave NT kernel below measured 1.16 ms forward / 1.62-1.66 ms dgrad against
@@ -270,6 +271,106 @@ __global__ __launch_bounds__(512) void fc_nt2_kernel(const __bf16* __restrict__ 
 }
 #undef FI_FC2_LOADS
 
+
+// ---------------------------------------------------------------- forward, hand-placed half-steps
+// 4 waves, 128 x 128 per wave (256 AGPR accumulators), 2 slots of k 64 (the same LDS images,
+// swizzle and k order as fc_nt_kernel, so the output is bit-identical). Each k 64 step = two
+// generated asm blocks (scripts/fc_asm_blocks.inc): block A = the first half's 64 MFMAs with the
+// second half's 16 fragment reads between them; the one barrier; block B = the second half's 64
+// MFMAs with the next step's first-half reads AND the step-after-next's 16 LDS-DMA pieces between
+// them -- one read and one DMA piece per 4 MFMAs, the placement hipBLASLt's loop uses.
+#include "fc_asm_blocks.inc"
+
+template <class Epi>
+__global__ __launch_bounds__(256) void fc_asm_kernel(const __bf16* __restrict__ X, const __bf16* __restrict__ Y, int NY,
+                                                     int K, int ntx, int ntiles, Epi epi) {
+    constexpr int BX = 256, BY = 256, BK = 64, NS = 2, SLOT = 65536, NST = 32;
+    __shared__ __attribute__((aligned(16))) char lds[NS * SLOT + Epi::kLdsFloats * 4];
+    const int lane = threadIdx.x & 63, w = wave_id(), G = lane >> 4;
+    const int wx = w >> 1, wy = w & 1;
+    const int NG = gridDim.x, lg = xcd_remap(blockIdx.x, NG);
+    const int nk = K / BK;
+    const int total = ((ntiles - 1 - lg) / NG + 1) * nk;
+    const uint32_t lbase = lds_addr(lds);
+    const float* lb = (const float*)(lds + NS * SLOT);
+    epi.init((float*)(lds + NS * SLOT), threadIdx.x, 256);
+    // per-lane DMA source offsets within a k-step (constant): piece j < 8 = X rows (w + 4j) * 8
+    // + lane / 8, j >= 8 = Y rows (w + 4(j - 8)) * 8 + lane / 8; chunk swizzled as the images
+    uint32_t vo[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int prow = (w + 4 * (j & 7)) * 8 + lane / 8;
+        vo[j] = (uint32_t)((prow * K + nt_chunk<BK>(lane % 8, prow) * 8) * 2);
+    }
+    // fragment read bases (bytes in LDS) per slot s and k-half h: X rows wx*128 + (lane & 15)
+    // (+16 f), Y rows wy*128 + (lane & 15) (+16 g); the row swizzle is the same for every f / g
+    const int r15 = lane & 15, sw = (r15 >> 1) & 7;
+    auto bxa = [&](int sl, int h) {
+        return lbase + (uint32_t)(sl * SLOT + (wx * 128 + r15) * 128 + (((h * 4 + G) ^ sw) << 4));
+    };
+    auto bya = [&](int sl, int h) {
+        return lbase + (uint32_t)(sl * SLOT + 32768 + (wy * 128 + r15) * 128 + (((h * 4 + G) ^ sw) << 4));
+    };
+    auto dma = [&](int j) {  // step j's 16 pieces into slot j % 2 (past the last step: 0-byte descriptors)
+        const bool live = j < total;
+        const int t = live ? lg + (j / nk) * NG : lg, kt = j % nk;
+        const int ty = t / ntx, tx = t - ty * ntx;
+        const fi_i32x4 rx = make_rsrc(X + (size_t)tx * BX * K, live ? (uint32_t)BX * K * 2 : 0u);
+        const fi_i32x4 ry = make_rsrc(Y + (size_t)ty * BY * K, live ? (uint32_t)min(BY, NY - ty * BY) * K * 2 : 0u);
+        const uint32_t mx = lbase + (uint32_t)((j % NS) * SLOT + w * 1024);
+        return std::make_tuple(rx, ry, (uint32_t)(kt * BK * 2), mx, mx + 32768u);
+    };
+    if (total <= 0) return;
+    {
+        auto [rx, ry, ko, mx, my] = dma(0);
+        fc_asm_dma(vo, rx, ry, ko, mx, my);
+    }
+    if (total > 1) {
+        auto [rx, ry, ko, mx, my] = dma(1);
+        fc_asm_dma(vo, rx, ry, ko, mx, my);
+        vm_wait_rt(16);
+    } else {
+        vm_wait_rt(0);
+    }
+    lds_barrier();
+    bf16x8 P[16], Q[16];
+    {
+        const uint32_t bx = bxa(0, 0), by = bya(0, 0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) P[j] = *(const bf16x8*)((const char*)lds + (bx - lbase) + j * 2048);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) P[8 + j] = *(const bf16x8*)((const char*)lds + (by - lbase) + j * 2048);
+    }
+    const int mytiles = total / nk;
+    int it = 0, last_epi = -(1 << 20);
+    for (int tile_it = 0; tile_it < mytiles; ++tile_it) {
+        f32x4 acc[64];
+#pragma unroll
+        for (int i = 0; i < 64; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int kt = 0; kt < nk; ++kt, ++it) {
+            // every step runs the same two blocks (a branch between block variants makes hipcc
+            // copy the accumulators through VGPRs at the merge): past the end, the reads fetch
+            // unused fragments and the DMA pieces carry 0-byte descriptors into a dead slot
+            const int sl = it % NS, sn = (it + 1) % NS;
+            fc_asm_mfma_reads(acc, P, Q, bxa(sl, 1), bya(sl, 1));
+            vm_wait_rt(last_epi == it - 1 ? NST : 0);
+            lds_barrier();
+            auto [rx, ry, ko, mx, my] = dma(it + 2);
+            fc_asm_mfma_reads_dma(acc, Q, P, bxa(sn, 0), bya(sn, 0), vo, rx, ry, ko, mx, my);
+        }
+        const int t = lg + tile_it * NG;
+        const int ty = t / ntx, tx = t - ty * ntx;
+        const int y0 = ty * BY;
+        const OutTile ot = epi.tile(y0, min(BY, NY - y0));
+        const int xw = tx * BX + wx * 128, yb = y0 + wy * 128 + (lane & 15);
+#pragma unroll
+        for (int g = 0; g < 8; ++g)
+#pragma unroll
+            for (int f = 0; f < 8; f += 2)
+                Epi::template pair<0>(ot, lb, xw + f * 16, yb + g * 16, G, acc[f * 8 + g], acc[(f + 1) * 8 + g]);
+        last_epi = it - 1;
+    }
+}
 }  // namespace fcg
 
 using namespace fcg;
@@ -298,6 +399,15 @@ static int fc_fwd2_impl(const __bf16* a3, const __bf16* wT, const float* bias, _
     FI_REQUIRE(rows > 0, "fc_fwd: rows must be positive");
     const int ntx = FCO / 256, nty = (rows + 255) / 256, nt = ntx * nty;
     hipLaunchKernelGGL((fc_nt2_kernel<EpiFwd>), dim3(std::min(nt, 256)), dim3(512), 0, s, wT, a3, rows, FCK, ntx, nt,
+                       EpiFwd{{h}, bias});
+    FI_HIP_CHECK(hipGetLastError());
+    return FI_OK;
+}
+
+static int fc_fwd_asm_impl(const __bf16* a3, const __bf16* wT, const float* bias, __bf16* h, int rows, hipStream_t s) {
+    FI_REQUIRE(rows > 0, "fc_fwd: rows must be positive");
+    const int ntx = FCO / 256, nty = (rows + 255) / 256, nt = ntx * nty;
+    hipLaunchKernelGGL((fc_asm_kernel<EpiFwd>), dim3(std::min(nt, 256)), dim3(256), 0, s, wT, a3, rows, FCK, ntx, nt,
                        EpiFwd{{h}, bias});
     FI_HIP_CHECK(hipGetLastError());
     return FI_OK;
