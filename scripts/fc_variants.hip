@@ -281,7 +281,7 @@ __global__ __launch_bounds__(512) void fc_nt2_kernel(const __bf16* __restrict__ 
 // them -- one read and one DMA piece per 4 MFMAs, the placement hipBLASLt's loop uses.
 #include "fc_asm_blocks.inc"
 
-template <class Epi>
+template <class Epi, int ABL = 0>  // ABL (timing-only ablations, wrong results): 1 = no vmcnt wait
 __global__ __launch_bounds__(256) void fc_asm_kernel(const __bf16* __restrict__ X, const __bf16* __restrict__ Y, int NY,
                                                      int K, int ntx, int ntiles, Epi epi) {
     constexpr int BX = 256, BY = 256, BK = 64, NS = 2, SLOT = 65536, NST = 32;
@@ -353,7 +353,7 @@ __global__ __launch_bounds__(256) void fc_asm_kernel(const __bf16* __restrict__ 
             // unused fragments and the DMA pieces carry 0-byte descriptors into a dead slot
             const int sl = it % NS, sn = (it + 1) % NS;
             fc_asm_mfma_reads(acc, P, Q, bxa(sl, 1), bya(sl, 1));
-            vm_wait_rt(last_epi == it - 1 ? NST : 0);
+            if constexpr (ABL != 1) vm_wait_rt(last_epi == it - 1 ? NST : 0);
             lds_barrier();
             auto [rx, ry, ko, mx, my] = dma(it + 2);
             fc_asm_mfma_reads_dma(acc, Q, P, bxa(sn, 0), bya(sn, 0), vo, rx, ry, ko, mx, my);
@@ -404,10 +404,11 @@ static int fc_fwd2_impl(const __bf16* a3, const __bf16* wT, const float* bias, _
     return FI_OK;
 }
 
+template <int ABL = 0>
 static int fc_fwd_asm_impl(const __bf16* a3, const __bf16* wT, const float* bias, __bf16* h, int rows, hipStream_t s) {
     FI_REQUIRE(rows > 0, "fc_fwd: rows must be positive");
     const int ntx = FCO / 256, nty = (rows + 255) / 256, nt = ntx * nty;
-    hipLaunchKernelGGL((fc_asm_kernel<EpiFwd>), dim3(std::min(nt, 256)), dim3(256), 0, s, wT, a3, rows, FCK, ntx, nt,
+    hipLaunchKernelGGL((fc_asm_kernel<EpiFwd, ABL>), dim3(std::min(nt, 256)), dim3(256), 0, s, wT, a3, rows, FCK, ntx, nt,
                        EpiFwd{{h}, bias});
     FI_HIP_CHECK(hipGetLastError());
     return FI_OK;
