@@ -371,6 +371,96 @@ __global__ __launch_bounds__(256) void fc_asm_kernel(const __bf16* __restrict__ 
         last_epi = it - 1;
     }
 }
+
+// ---------------------------------------------------------------- forward, k-half-split ring
+// fc_asm_kernel with each 64-KiB step slot split into two k-32 half-slots ([256 rows][32 k] X and
+// Y images, 64-B rows, swizzle nt_chunk<32>), each freed by its own barrier (two per step) and
+// refilled three half-steps ahead: block A(it) = the first half's MFMAs + the second half's
+// reads + step it+2's FIRST half DMA; block B(it) = the second half's MFMAs + step it+1's first
+// half reads + step it+2's SECOND half DMA. Every barrier waits with 16 pieces still in flight.
+template <class Epi>
+__global__ __launch_bounds__(256) void fc_asm2_kernel(const __bf16* __restrict__ X, const __bf16* __restrict__ Y, int NY,
+                                                      int K, int ntx, int ntiles, Epi epi) {
+    constexpr int BX = 256, BY = 256, BK = 64, HS = 32768, NST = 32;  // half-slot bytes
+    __shared__ __attribute__((aligned(16))) char lds[4 * HS + Epi::kLdsFloats * 4];
+    const int lane = threadIdx.x & 63, w = wave_id(), G = lane >> 4;
+    const int wx = w >> 1, wy = w & 1;
+    const int NG = gridDim.x, lg = xcd_remap(blockIdx.x, NG);
+    const int nk = K / BK;
+    const int total = ((ntiles - 1 - lg) / NG + 1) * nk;
+    const uint32_t lbase = lds_addr(lds);
+    const float* lb = (const float*)(lds + 4 * HS);
+    epi.init((float*)(lds + 4 * HS), threadIdx.x, 256);
+    // piece j < 4: X rows (w + 4j) * 16 + lane / 4; j >= 4: Y rows (w + 4(j - 4)) * 16 + lane / 4
+    uint32_t vo[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int prow = (w + 4 * (j & 3)) * 16 + lane / 4;
+        vo[j] = (uint32_t)((prow * K + nt_chunk<32>(lane % 4, prow) * 8) * 2);
+    }
+    const int r15 = lane & 15, sw = nt_chunk<32>(G, r15);  // chunk position of k-group G
+    auto bxa = [&](int hs) { return lbase + (uint32_t)(hs * HS + (wx * 128 + r15) * 64 + (sw << 4)); };
+    auto bya = [&](int hs) { return lbase + (uint32_t)(hs * HS + 16384 + (wy * 128 + r15) * 64 + (sw << 4)); };
+    auto dma = [&](int j, int h) {  // half h of step j into half-slot (j % 2) * 2 + h
+        const bool live = j < total;
+        const int t = live ? lg + (j / nk) * NG : lg, kt = j % nk;
+        const int ty = t / ntx, tx = t - ty * ntx;
+        const fi_i32x4 rx = make_rsrc(X + (size_t)tx * BX * K, live ? (uint32_t)BX * K * 2 : 0u);
+        const fi_i32x4 ry = make_rsrc(Y + (size_t)ty * BY * K, live ? (uint32_t)min(BY, NY - ty * BY) * K * 2 : 0u);
+        const uint32_t mx = lbase + (uint32_t)(((j % 2) * 2 + h) * HS + w * 1024);
+        return std::make_tuple(rx, ry, (uint32_t)(kt * BK * 2 + h * 64), mx, mx + 16384u);
+    };
+    if (total <= 0) return;
+    for (int j = 0; j < 2; ++j)
+        for (int h = 0; h < 2; ++h) {
+            auto [rx, ry, ko, mx, my] = dma(j, h);
+            fc_asm2_dma(vo, rx, ry, ko, mx, my);
+        }
+    vm_wait_rt(24);  // step 0's first half landed
+    lds_barrier();
+    bf16x8 P[16], Q[16];
+    {
+        const uint32_t bx = bxa(0), by = bya(0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) P[j] = *(const bf16x8*)((const char*)lds + (bx - lbase) + j * 1024);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) P[8 + j] = *(const bf16x8*)((const char*)lds + (by - lbase) + j * 1024);
+    }
+    const int mytiles = total / nk;
+    int it = 0, last_epi = -(1 << 20);
+    for (int tile_it = 0; tile_it < mytiles; ++tile_it) {
+        f32x4 acc[64];
+#pragma unroll
+        for (int i = 0; i < 64; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int kt = 0; kt < nk; ++kt, ++it) {
+            const int sl = it % 2, sn = (it + 1) % 2;
+            const int behind = 16 + (last_epi == it - 1 ? NST : 0);  // pieces (+ stores) newer than the one waited for
+            vm_wait_rt(behind);  // step it's second half landed; everyone is done with half-slot sl*2
+            lds_barrier();
+            {
+                auto [rx, ry, ko, mx, my] = dma(it + 2, 0);
+                fc_asm2_mfma_reads_dma(acc, P, Q, bxa(sl * 2 + 1), bya(sl * 2 + 1), vo, rx, ry, ko, mx, my);
+            }
+            vm_wait_rt(behind);  // step it+1's first half landed; everyone is done with half-slot sl*2+1
+            lds_barrier();
+            {
+                auto [rx, ry, ko, mx, my] = dma(it + 2, 1);
+                fc_asm2_mfma_reads_dma(acc, Q, P, bxa(sn * 2), bya(sn * 2), vo, rx, ry, ko, mx, my);
+            }
+        }
+        const int t = lg + tile_it * NG;
+        const int ty = t / ntx, tx = t - ty * ntx;
+        const int y0 = ty * BY;
+        const OutTile ot = epi.tile(y0, min(BY, NY - y0));
+        const int xw = tx * BX + wx * 128, yb = y0 + wy * 128 + (lane & 15);
+#pragma unroll
+        for (int g = 0; g < 8; ++g)
+#pragma unroll
+            for (int f = 0; f < 8; f += 2)
+                Epi::template pair<0>(ot, lb, xw + f * 16, yb + g * 16, G, acc[f * 8 + g], acc[(f + 1) * 8 + g]);
+        last_epi = it - 1;
+    }
+}
 }  // namespace fcg
 
 using namespace fcg;
@@ -409,6 +499,15 @@ static int fc_fwd_asm_impl(const __bf16* a3, const __bf16* wT, const float* bias
     FI_REQUIRE(rows > 0, "fc_fwd: rows must be positive");
     const int ntx = FCO / 256, nty = (rows + 255) / 256, nt = ntx * nty;
     hipLaunchKernelGGL((fc_asm_kernel<EpiFwd, ABL>), dim3(std::min(nt, 256)), dim3(256), 0, s, wT, a3, rows, FCK, ntx, nt,
+                       EpiFwd{{h}, bias});
+    FI_HIP_CHECK(hipGetLastError());
+    return FI_OK;
+}
+
+static int fc_fwd_asm2_impl(const __bf16* a3, const __bf16* wT, const float* bias, __bf16* h, int rows, hipStream_t s) {
+    FI_REQUIRE(rows > 0, "fc_fwd: rows must be positive");
+    const int ntx = FCO / 256, nty = (rows + 255) / 256, nt = ntx * nty;
+    hipLaunchKernelGGL((fc_asm2_kernel<EpiFwd>), dim3(std::min(nt, 256)), dim3(256), 0, s, wT, a3, rows, FCK, ntx, nt,
                        EpiFwd{{h}, bias});
     FI_HIP_CHECK(hipGetLastError());
     return FI_OK;
