@@ -85,6 +85,7 @@ int main(int argc, char** argv) {
     FWSV("ws 256x128 c2x2 l4 ntY", 256, 128, 2, 2, 4, 8);
     add("fwd  4 waves, hand-placed asm half-steps", 0, [&](hipStream_t st, int k) { return fc_fwd_asm_impl(a3, wT, bias, h[k], R, st); }, h[0], h[1], (size_t)R * FCO * 2);
     add("fwd  asm, k-half-split ring", 0, [&](hipStream_t st, int k) { return fc_fwd_asm2_impl(a3, wT, bias, h[k], R, st); }, h[0], h[1], (size_t)R * FCO * 2);
+    add("fwd  asm, one W half per XCD", 0, [&](hipStream_t st, int k) { return fc_fwd_asm_impl<2>(a3, wT, bias, h[k], R, st); }, h[0], h[1], (size_t)R * FCO * 2);
     add("fwd  asm, no vmcnt wait (timing only)", 0, [&](hipStream_t st, int k) { return fc_fwd_asm_impl<1>(a3, wT, bias, h[k], R, st); }, h[0], h[1], (size_t)R * FCO * 2);
     add("fwd  midbar ntY, one DMA asm block per step", 0, [&](hipStream_t st, int k) { return fc_fwd2_impl(a3, wT, bias, h[k], R, st); }, h[0], h[1], (size_t)R * FCO * 2);
     DGV("224x256 w1x8 bk64 ns2 prio ntst", 224, 256, 1, 8, 64, 2, 1 | 2);

@@ -281,7 +281,7 @@ __global__ __launch_bounds__(512) void fc_nt2_kernel(const __bf16* __restrict__ 
 // them -- one read and one DMA piece per 4 MFMAs, the placement hipBLASLt's loop uses.
 #include "fc_asm_blocks.inc"
 
-template <class Epi, int ABL = 0>  // ABL (timing-only ablations, wrong results): 1 = no vmcnt wait
+template <class Epi, int ABL = 0>  // ABL: 1 = no vmcnt wait (timing only, wrong results); 2 = one W half per XCD (tile map)
 __global__ __launch_bounds__(256) void fc_asm_kernel(const __bf16* __restrict__ X, const __bf16* __restrict__ Y, int NY,
                                                      int K, int ntx, int ntiles, Epi epi) {
     constexpr int BX = 256, BY = 256, BK = 64, NS = 2, SLOT = 65536, NST = 32;
@@ -290,7 +290,21 @@ __global__ __launch_bounds__(256) void fc_asm_kernel(const __bf16* __restrict__ 
     const int wx = w >> 1, wy = w & 1;
     const int NG = gridDim.x, lg = xcd_remap(blockIdx.x, NG);
     const int nk = K / BK;
-    const int total = ((ntiles - 1 - lg) / NG + 1) * nk;
+    // tile of round i: default t = lg + i*NG (both W halves on every XCD); ABL 2 (grid 256, ntx 2):
+    // XCD x = b % 8 keeps W half x & 1 and walks frame tiles i*128 + (x >> 1)*32 + b / 8
+    const int b8 = blockIdx.x % 8, j8 = blockIdx.x / 8, nty = ntiles / ntx;
+    auto tile = [&](int i, int& tx, int& ty) {
+        if constexpr (ABL == 2) {
+            tx = b8 & 1;
+            ty = i * 128 + (b8 >> 1) * 32 + j8;
+        } else {
+            const int t = lg + i * NG;
+            ty = t / ntx;
+            tx = t - ty * ntx;
+        }
+    };
+    const int first = (b8 >> 1) * 32 + j8;
+    const int total = (ABL == 2 ? (first < nty ? (nty - first + 127) / 128 : 0) : (ntiles - 1 - lg) / NG + 1) * nk;
     const uint32_t lbase = lds_addr(lds);
     const float* lb = (const float*)(lds + NS * SLOT);
     epi.init((float*)(lds + NS * SLOT), threadIdx.x, 256);
@@ -313,8 +327,9 @@ __global__ __launch_bounds__(256) void fc_asm_kernel(const __bf16* __restrict__ 
     };
     auto dma = [&](int j) {  // step j's 16 pieces into slot j % 2 (past the last step: 0-byte descriptors)
         const bool live = j < total;
-        const int t = live ? lg + (j / nk) * NG : lg, kt = j % nk;
-        const int ty = t / ntx, tx = t - ty * ntx;
+        const int kt = j % nk;
+        int tx, ty;
+        tile(live ? j / nk : 0, tx, ty);
         const fi_i32x4 rx = make_rsrc(X + (size_t)tx * BX * K, live ? (uint32_t)BX * K * 2 : 0u);
         const fi_i32x4 ry = make_rsrc(Y + (size_t)ty * BY * K, live ? (uint32_t)min(BY, NY - ty * BY) * K * 2 : 0u);
         const uint32_t mx = lbase + (uint32_t)((j % NS) * SLOT + w * 1024);
@@ -358,8 +373,8 @@ __global__ __launch_bounds__(256) void fc_asm_kernel(const __bf16* __restrict__ 
             auto [rx, ry, ko, mx, my] = dma(it + 2);
             fc_asm_mfma_reads_dma(acc, Q, P, bxa(sn, 0), bya(sn, 0), vo, rx, ry, ko, mx, my);
         }
-        const int t = lg + tile_it * NG;
-        const int ty = t / ntx, tx = t - ty * ntx;
+        int tx, ty;
+        tile(tile_it, tx, ty);
         const int y0 = ty * BY;
         const OutTile ot = epi.tile(y0, min(BY, NY - y0));
         const int xw = tx * BX + wx * 128, yb = y0 + wy * 128 + (lane & 15);
