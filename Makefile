@@ -7,7 +7,7 @@ LIBDIR := freeimpala_amd/lib
 OBJDIR := build/obj
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude -I$(CSRC) -Wall -Wno-unused-result -Wno-unused-value \
             -munsafe-fp-atomics
-SRCS := $(CSRC)/farmer.hip $(CSRC)/vtrace.hip $(CSRC)/gemm_f32.hip $(CSRC)/misc.hip $(CSRC)/atari.hip $(CSRC)/atari_fr.hip $(CSRC)/fc_gemm.hip $(CSRC)/fc_blaslt.cpp $(CSRC)/learner.cpp
+SRCS := $(CSRC)/farmer.hip $(CSRC)/vtrace.hip $(CSRC)/gemm_f32.hip $(CSRC)/misc.hip $(CSRC)/atari.hip $(CSRC)/atari_fr.hip $(CSRC)/fc_gemm.hip $(CSRC)/learner.cpp
 OBJS := $(patsubst $(CSRC)/%,$(OBJDIR)/%.o,$(SRCS))
 HDRS := $(wildcard $(CSRC)/*.h) include/fi_learner.h include/fi_farmer.h
 
@@ -23,7 +23,7 @@ $(OBJDIR)/%.cpp.o: $(CSRC)/%.cpp $(HDRS)
 
 $(LIBDIR)/libfi_learner.so: $(OBJS)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -L/opt/rocm/lib -lrccl -lhipblaslt -Wl,-rpath,/opt/rocm/lib
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 oracle:
 	$(MAKE) -s -C oracle

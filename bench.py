@@ -219,7 +219,7 @@ def main():
 
     ws, rank, local = dist_env()
     N = max(ws, 1)
-    # the learner library first: it then binds the image's ROCm 7.2 runtime, hipBLASLt and RCCL
+    # the learner library first: it then binds the image's ROCm 7.2 runtime and RCCL
     # (what it is built against, and what the tests and smoke() load); imported first, torch's
     # bundled ROCm 7.0 copies would take those sonames. torch is only the gloo launcher here
     # and never touches the GPU.
@@ -232,7 +232,8 @@ def main():
     if ws > 1:
         dist.init_process_group("gloo", rank=rank, world_size=ws)
 
-    from freeimpala_amd.launch import broadcast_bytes, max_over_ranks, shard_columns
+    from freeimpala_amd.launch import (broadcast_bytes, data_parallel_fields, gather_objects, max_over_ranks,
+                                       shard_columns)
     from freeimpala_amd.learner import DeviceLearner
 
     T, B, A = args.seq_len, args.batch, args.num_actions
@@ -262,6 +263,7 @@ def main():
     L.sync()
     barrier()
     elapsed = time.perf_counter() - t0
+    own_ms_per_step = 1000.0 * elapsed / args.steps  # this rank's own clock, before the max
     if ws > 1:
         elapsed = max_over_ranks(elapsed)
     ms_per_step = 1000.0 * elapsed / args.steps
@@ -279,6 +281,17 @@ def main():
     vt_cold_ms = L.replay_vtrace(VT_REPLAYS, sets=VT_COLD_SETS)
     vt_warm_ms = L.replay_vtrace(VT_REPLAYS, sets=1)
     st = L.step_resident(stats=True)
+
+    # N > 1: every rank's own ms/step and exposed all-reduce wait, the bytes all-reduced per step
+    dp = None
+    if ws > 1:
+        comm = L.comm_info()
+        dp = data_parallel_fields(gather_objects({"ms_per_step": own_ms_per_step,
+                                                  "allreduce_ms": phases.get("allreduce", 0.0)}),
+                                  grad_bytes=4 * L.param_count,
+                                  buckets=comm["buckets_last_step"] if comm["nranks"] > 1 else None)
+        if os.environ.get("FI_BENCH_NO_COMM"):
+            dp["note"] = "FI_BENCH_NO_COMM rehearsal: no communicator, nothing was all-reduced"
 
     work = kernel_work(args.arch, T, B, A)
     # Counter fields from the committed rocprofv3 PMC summaries (scripts/pmc_pass.sh: HBM bytes
@@ -342,6 +355,8 @@ def main():
         "comm": L.comm_info(),
         "counters_build": counters_build,
     }
+    if dp is not None:
+        result["data_parallel"] = dp
     if rank == 0 and N == 1 and not args.no_cpu_baseline:
         # every core this process may use: the box's OMP_NUM_THREADS share when set (16 per GPU
         # on the pool's boxes, whose nproc counts the whole host), else the affinity mask

@@ -35,8 +35,8 @@ def source_hash() -> str:
 
 # run-time switches that change which kernels the learner step launches, or how: a counter pass
 # taken under one setting says nothing about a bench line timed under another
-KERNEL_ENV = ("FI_FR_GRID", "FI_FC_OWN", "FI_BLT_NO_SWEEP", "FI_KEEP_DA1", "FI_BWD_UNFUSED", "FI_FWD_UNFUSED",
-              "FI_A1_NHWC", "FI_ATARI_GENERIC", "FI_DETERMINISTIC")
+KERNEL_ENV = ("FI_FR_GRID", "FI_KEEP_DA1", "FI_BWD_UNFUSED", "FI_FWD_UNFUSED",
+              "FI_A1_NHWC", "FI_ATARI_GENERIC")
 
 
 def rocm_version() -> str:

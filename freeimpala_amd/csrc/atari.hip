@@ -23,7 +23,6 @@
 #include <vector>
 
 #include "atari.h"
-#include "fc_blaslt.h"
 #include "fi_common.h"
 #include "kernels.h"
 
@@ -731,7 +730,6 @@ struct AtariImpl {
     bool a1_planar = true; // fused fwd + bwd: a1 stored in conv21's image order (FI_A1_NHWC=1 -> NHWC)
     int fr_grid = 256;     // persistent frame-resident workgroups, 1 per CU (FI_FR_GRID=g: tests put
                            // many frames on each workgroup at small N to reach the steady state)
-    FcBlasLt* fc = nullptr;  // fc forward / dgrad on hipBLASLt (null with FI_FC_OWN=1: fc_gemm.hip)
 };
 
 int conv1_fwd_fr_launch(const uint8_t* frames, const __bf16* w1t, const float* bias, __bf16* a1,
@@ -814,18 +812,9 @@ AtariNet* atari_create(int B, int T, int A) {
         atari_destroy(n);
         return nullptr;
     }
-    if (!std::getenv("FI_FC_OWN")) {
-        I->fc = fc_blaslt_create((int)N, I->a3, I->wb.fcB, I->dh, I->h, I->da3, s0);
-        if (!I->fc) {  // fc_blaslt_create set the error
-            (void)hipStreamDestroy(s0);
-            atari_destroy(n);
-            return nullptr;
-        }
-    }
     // the data-gradient rows T*B.. (dh, da3, da2, da1) are never written by the backward (it walks
-    // T*B frames): zeros, so those tensors read as the exact gradients (0) there -- after the
-    // library's algorithm timing, which fills dh with test data -- on the creation stream and
-    // waited for (no legacy-stream memset racing the learner's stream)
+    // T*B frames): zeros, so those tensors read as the exact gradients (0) there -- on the
+    // creation stream and waited for (no legacy-stream memset racing the learner's stream)
     if (hipMemsetAsync(I->dh, 0, N * 512 * sizeof(__bf16), s0) != hipSuccess ||
         hipMemsetAsync(I->da3, 0, N * 3136 * sizeof(__bf16), s0) != hipSuccess ||
         hipMemsetAsync(I->da2, 0, N * 81 * 64 * sizeof(__bf16), s0) != hipSuccess ||
@@ -843,7 +832,6 @@ void atari_destroy(AtariNet* n) {
     if (!n) return;
     AtariImpl* I = impl(n);
     if (I) {
-        fc_blaslt_destroy(I->fc);
         for (void* p : I->allocs) (void)hipFree(p);
         delete I;
     }
@@ -893,8 +881,7 @@ int atari_forward(AtariNet* n, const uint8_t* frames, float* logits, float* valu
     if (rc) return rc;
     {
         TagScope ts(tg, "fc_fwd");
-        rc = I->fc ? fc_blaslt_forward(I->fc, I->a3, I->wb.fcB, p + o.fcb, I->h, s)
-                   : fc_fwd_launch(I->a3, I->wb.fcT, p + o.fcb, I->h, N, s);
+        rc = fc_fwd_launch(I->a3, I->wb.fcT, p + o.fcb, I->h, N, s);
     }
     if (rc) return rc;
     { TagScope ts(tg, "heads_fwd"); rc = gemm<128, 32, 4, 1>(RowsBf16{I->h, N, FCO}, RowsBf16{I->wb.hT, HP, FCO},
@@ -909,7 +896,7 @@ int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, con
     // the last B frames (t = T) only give the bootstrap value: their dlogits do not exist and
     // their dvalue is 0, so every gradient they would add is exactly 0 -- the frame-resident
     // backward kernels walk the first T*B frames only (dh rows T*B.. stay the zeros written at
-    // creation, for the library fc dgrad that reads all N rows)
+    // creation, for the generic path's conv GEMMs that read all N rows)
     const int Nb = I->TB;
     const Offsets& o = I->off;
     using namespace geo;
@@ -943,8 +930,7 @@ int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, con
     // buckets in reverse layer order: fc + heads (95 % of the gradient bytes) reduce while
     // fc dgrad, conv3 and conv2/conv1 backward run
     if (gr && (rc = gr->ready(o.fcw, o.total - o.fcw))) return rc;
-    FI_A("fc_dgrad", I->fc ? fc_blaslt_dgrad(I->fc, I->dh, I->wb.fcB, I->da3, s)
-                           : fc_dgrad_launch(I->dh, I->wb.fcB, I->da3, I->fr ? Nb : N, s));  // the GEMM path reads all N
+    FI_A("fc_dgrad", fc_dgrad_launch(I->dh, I->wb.fcB, I->da3, I->fr ? Nb : N, s));  // the GEMM path reads all N
     // conv3: wgrad [576][64] + bias, dgrad -> da2 (masked by a2)
     if (I->fr) {
         const int grid = std::min(N, I->fr_grid);

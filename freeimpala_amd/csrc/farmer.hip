@@ -485,13 +485,16 @@ __device__ __forceinline__ bool sm_grid_sync(const SmSync& sy, unsigned phase, i
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_fetch_add(sy.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned target = sy.base + phase * (unsigned)gridDim.x;
-        int ok = 1;
-        for (unsigned spins = 0; (int)(__hip_atomic_load(sy.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0;) {
+        // a status already set (an earlier barrier of this launch or of an earlier launch gave up:
+        // the counter no longer matches the host's base) ends the wait at once
+        int ok = __hip_atomic_load(sy.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
+        for (unsigned spins = 0; ok && (int)(__hip_atomic_load(sy.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0;) {
             __builtin_amdgcn_s_sleep(2);
             if (++spins > (1u << 22)) {
                 __hip_atomic_fetch_or(sy.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 ok = 0;
-                break;
+            } else if ((spins & 63) == 0 && __hip_atomic_load(sy.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                ok = 0;  // another workgroup gave up
             }
         }
         if (ok && __hip_atomic_load(sy.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) ok = 0;
@@ -736,9 +739,16 @@ __global__ void copy_kernel(const float* __restrict__ src, float* __restrict__ d
 // torch.optim single-tensor update formulas in fp32 (torch/optim/adam.py, sgd.py):
 //   AdamW: p *= 1 - lr wd;  m = lerp(m, g, 1 - b1);  v = v b2 + (1 - b2) g g
 //   p += -(lr / bc1) m / (sqrt(v) / sqrt(bc2) + eps);   Adam with wd: g += wd p first;  SGD: p += -lr g
+// status (fused torso only, else null): sync[1] nonzero = a grid barrier of this or an earlier
+// fused launch gave up, so the gradient is partial -- the update is skipped (parameters and
+// moments untouched) and counted in sync[2], which the host subtracts from its step count
 __global__ void farmer_opt_kernel(int kind, float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                                   float* __restrict__ v, size_t n, float lr, float wd, float b1, float b2, float eps,
-                                  float neg_step_size, float bc2_sqrt, float decay) {
+                                  float neg_step_size, float bc2_sqrt, float decay, unsigned* status) {
+    if (status && __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) __hip_atomic_fetch_add(status + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
         float pi = p[i], gi = g[i];
         if (kind == FI_FOPT_SGD) {
@@ -782,7 +792,8 @@ struct fi_farmer {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     hipEvent_t pe[4] = {};  // profiling: around lstm_fwd, around lstm_bwd
     bool small = false;             // B <= 64: fused torso kernels (mlp_*_small_kernel)
-    unsigned* sync = nullptr;       // [0] grid-barrier counter, [1] status (own 64-B allocation)
+    unsigned* sync = nullptr;       // [0] grid-barrier counter, [1] status, [2] updates skipped since
+                                    // the status was set (own 64-B allocation)
     unsigned sync_base = 0;         // counter value at the start of the next fused launch
     bool profiling = false;
     double prof_fwd = 0.0, prof_bwd = 0.0;
@@ -919,7 +930,8 @@ static int optimize(fi_farmer* f) {
     const float decay = (float)(1.0 - (double)c.lr * (double)c.weight_decay);
     const size_t n = f->off.total;
     hipLaunchKernelGGL(farmer_opt_kernel, dim3(1024), dim3(256), 0, f->stream, c.optimizer, f->params, f->grads, f->m,
-                       f->v, n, c.lr, c.weight_decay, c.beta1, c.beta2, c.eps, neg_ss, bc2s, decay);
+                       f->v, n, c.lr, c.weight_decay, c.beta1, c.beta2, c.eps, neg_ss, bc2s, decay,
+                       f->small ? f->sync + 1 : nullptr);
     FI_HIP_CHECK(hipGetLastError());
     return FI_OK;
 }
@@ -931,6 +943,26 @@ static int stage_inputs(fi_farmer* f, const float* z, const float* x, const floa
     if (x && x != f->x) FI_HIP_CHECK(hipMemcpyAsync(f->x, x, nx * 4, k, f->stream));
     if (y && y != f->y) FI_HIP_CHECK(hipMemcpyAsync(f->y, y, ny * 4, k, f->stream));
     return FI_OK;
+}
+
+// Fused torso only: did a grid barrier give up since the last check? The step that timed out
+// and every fused step after it (until this check) left their gradients partial and skipped their
+// optimizer updates (farmer_opt_kernel), so the parameters are those of the last good step. The
+// check reports it once, takes the skipped updates off the step count (Adam's bias correction
+// stays that of the updates actually applied) and resets the counter, status and base, so the
+// handle steps normally again. Synchronises the stream.
+static int fused_status(fi_farmer* f, const char* what) {
+    if (!f->small) return FI_OK;
+    unsigned st[3] = {0, 0, 0};
+    FI_HIP_CHECK(hipMemcpyAsync(st, f->sync, sizeof(st), hipMemcpyDeviceToHost, f->stream));
+    FI_HIP_CHECK(hipStreamSynchronize(f->stream));
+    if (st[1] == 0) return FI_OK;
+    f->step -= (int)std::min<unsigned>(st[2], (unsigned)f->step);
+    FI_HIP_CHECK(hipMemsetAsync(f->sync, 0, 64, f->stream));
+    FI_HIP_CHECK(hipStreamSynchronize(f->stream));
+    f->sync_base = 0;
+    return fail(FI_ERR_HIP, std::string(what) + ": a grid barrier of the fused torso timed out; " +
+                                std::to_string(st[2]) + " optimizer update(s) skipped, parameters are those of the last good step");
 }
 
 extern "C" size_t fi_farmer_param_count(void) { return Off().total; }
@@ -992,6 +1024,19 @@ extern "C" int fi_farmer_create(const fi_farmer_config* cfg, fi_farmer** out) {
     int cus = 0;
     if (rc == FI_OK && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, f->dev) != hipSuccess) cus = 0;
     f->small = f->B <= SM_MAXB && cus >= SM_WG && !std::getenv("FI_FARMER_UNFUSED");
+    if (f->small && rc == FI_OK) {
+        // and the occupancy calculator must agree that SM_WG of each fused kernel fit at once
+        // (an ordinary launch guarantees no residency; other kernels on the device can still
+        // delay it, in which case a barrier times out and the step reports it, fused_status)
+        int per_cu = 0, worst = 1 << 30;
+        const void* ks[4] = {(const void*)mlp_fwd_small_kernel<1>, (const void*)mlp_fwd_small_kernel<2>,
+                             (const void*)mlp_bwd_small_kernel<1>, (const void*)mlp_bwd_small_kernel<2>};
+        for (const void* k : ks) {
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, 0) != hipSuccess) per_cu = 0;
+            worst = std::min(worst, per_cu);
+        }
+        f->small = (long)worst * cus >= SM_WG;
+    }
     if (rc == FI_OK && hipStreamCreateWithFlags(&f->stream, hipStreamNonBlocking) != hipSuccess)
         rc = fail(FI_ERR_HIP, "farmer_create: hipStreamCreate failed");
     if (rc == FI_OK && (hipEventCreate(&f->e0) != hipSuccess || hipEventCreate(&f->e1) != hipSuccess))
@@ -1013,6 +1058,9 @@ extern "C" int fi_farmer_create(const fi_farmer_config* cfg, fi_farmer** out) {
         fi_farmer_destroy(f);
         return rc;
     }
+    // fault injection for the containment test only: a skewed barrier base makes the first fused
+    // launch's barriers unreachable, so they time out (tests/test_gpu_farmer.py)
+    if (const char* k = std::getenv("FI_FARMER_SYNC_SKEW")) f->sync_base = (unsigned)std::atoi(k);
     *out = f;
     return FI_OK;
 }
@@ -1050,12 +1098,14 @@ static int d2h(fi_farmer* f, const float* src, float* host, size_t n) {
 
 extern "C" int fi_farmer_get_params(fi_farmer* f, float* host, size_t n) {
     FI_REQUIRE(f && host && n == f->off.total, "farmer_get_params: need fi_farmer_param_count() floats");
-    return d2h(f, f->params, host, n);
+    FI_TRY(d2h(f, f->params, host, n));
+    return fused_status(f, "farmer_get_params");
 }
 
 extern "C" int fi_farmer_get_grads(fi_farmer* f, float* host, size_t n) {
     FI_REQUIRE(f && host && n == f->off.total, "farmer_get_grads: need fi_farmer_param_count() floats");
-    return d2h(f, f->grads, host, n);
+    FI_TRY(d2h(f, f->grads, host, n));
+    return fused_status(f, "farmer_get_grads");
 }
 
 extern "C" int fi_farmer_train_step(fi_farmer* f, const float* z, const float* x, const float* targets,
@@ -1080,18 +1130,15 @@ extern "C" int fi_farmer_train_step(fi_farmer* f, const float* z, const float* x
     if (values) FI_HIP_CHECK(hipMemcpyAsync(values, f->val, (size_t)f->B * 4, hipMemcpyDeviceToHost, f->stream));
     if (out) {
         double l = 0.0;
-        unsigned st = 0;
         FI_HIP_CHECK(hipMemcpyAsync(&l, f->loss, sizeof(double), hipMemcpyDeviceToHost, f->stream));
-        if (f->small) FI_HIP_CHECK(hipMemcpyAsync(&st, f->sync + 1, sizeof(st), hipMemcpyDeviceToHost, f->stream));
-        FI_HIP_CHECK(hipStreamSynchronize(f->stream));
-        FI_REQUIRE(st == 0, "farmer_train_step: a grid barrier of the fused torso timed out");
+        FI_TRY(fused_status(f, "farmer_train_step"));
         float ms = 0.f;
         FI_HIP_CHECK(hipEventElapsedTime(&ms, f->e0, f->e1));
         out->loss = l;
         out->step_ms = ms;
         out->step = f->step;
     } else if (values) {
-        FI_HIP_CHECK(hipStreamSynchronize(f->stream));
+        FI_TRY(fused_status(f, "farmer_train_step"));
     }
     return FI_OK;
 }
@@ -1102,12 +1149,7 @@ extern "C" int fi_farmer_forward(fi_farmer* f, const float* z, const float* x, i
     FI_TRY(stage_inputs(f, z, x, nullptr, inputs_on_device));
     FI_TRY(forward(f));
     FI_TRY(d2h(f, f->val, values, (size_t)f->B));
-    if (f->small) {
-        unsigned st = 0;
-        FI_TRY(d2h(f, (const float*)(f->sync + 1), (float*)&st, 1));
-        FI_REQUIRE(st == 0, "farmer_forward: a grid barrier of the fused torso timed out");
-    }
-    return FI_OK;
+    return fused_status(f, "farmer_forward");
 }
 
 extern "C" int fi_farmer_tensor(fi_farmer* f, const char* name, void** ptr, size_t* bytes) {

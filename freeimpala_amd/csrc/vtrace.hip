@@ -1024,12 +1024,10 @@ static bool lds_supported(int A, int B) { return B % 8 == 0 && A % 2 == 0 && A >
 
 template <int A>
 static void launch_str(const VtArgs& a, int nblk, hipStream_t s) {
-    // more than 64 KB of dynamic LDS: raise the kernel's limit once (thread-safe, per instantiation)
-    static std::once_flag once;
-    std::call_once(once, [] {
-        (void)hipFuncSetAttribute((const void*)vtrace_stream_kernel<A>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-    });
+    // more than 64 KB of dynamic LDS: raise the kernel's limit on the calling thread's current
+    // device before every launch (cheap; a once-per-process flag would only cover the first device)
+    (void)hipFuncSetAttribute((const void*)vtrace_stream_kernel<A>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
     hipLaunchKernelGGL(vtrace_stream_kernel<A>, dim3(nblk), dim3(VtStr<A>::NT), VtStr<A>::lds_bytes(a.T), s, a);
 }
 // persistent grid of the streaming kernel: one workgroup per CU (132 KB of LDS at T = 100)
@@ -1044,8 +1042,11 @@ static int str_lds_bytes(int T, int A) {
     const int logp = (T * 4 * A * 4 + 1023) / 1024, scp = (T * 16 + 1023) / 1024, valp = ((T + 1) * 16 + 1023) / 1024;
     return 2 * 1024 * (2 * logp + 3 * scp + valp) + 8 * 4 * 2 * 4;
 }
+// the dlogits tile leaves in 4 rounds of NT = 512 pieces of 16 B (VtStr::NST counts them), so
+// T * PPR = T * A pieces must fit 2,048 (T <= 113 at A = 18, T <= 102 at A = 20)
 static bool str_supported(int T, int A, int B) {
-    return B % 4 == 0 && A % 2 == 0 && A >= 2 && A <= 20 && T <= VtStr<2>::TMAX && str_lds_bytes(T, A) <= 160 * 1024;
+    return B % 4 == 0 && A % 2 == 0 && A >= 2 && A <= 20 && T <= VtStr<2>::TMAX && T * A <= 4 * VtStr<2>::NT &&
+           str_lds_bytes(T, A) <= 160 * 1024;
 }
 
 int vtrace_launch(int variant, int T, int B, int A, const float* pi, const float* mu,
@@ -1100,7 +1101,7 @@ int vtrace_launch(int variant, int T, int B, int A, const float* pi, const float
     }
     if (variant == 4) {
         FI_REQUIRE(str_supported(T, A, B) && fits32,
-                   "vtrace: streaming kernel needs B%4==0, even A<=20 and the whole sequence of 4 columns in 80 KB of LDS");
+                   "vtrace: streaming kernel needs B%4==0, even A<=20, T*A<=2048 and the whole sequence of 4 columns in 160 KB of LDS");
         FI_REQUIRE(vs && adv, "vtrace: streaming kernel writes vs and pg_adv (non-null)");
         FI_REQUIRE(((uintptr_t)pi | (uintptr_t)mu | (uintptr_t)dlog) % 16 == 0 &&
                    ((uintptr_t)act | (uintptr_t)rew | (uintptr_t)disc | (uintptr_t)val) % 16 == 0,

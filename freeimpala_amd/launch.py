@@ -8,7 +8,10 @@ here so that it can be exercised on CPU with the gloo backend (tests/test_dist_g
   * broadcast_bytes     -- the RCCL unique id from rank 0 to every rank (gloo tensors);
   * max_over_ranks      -- the bench's max-over-ranks wall time;
   * split_entries       -- a SharedBuffer::readBatch result (M host entries) split into the
-                           N contiguous per-GPU shards (reference data_structures.h:267-300).
+                           N contiguous per-GPU shards (reference data_structures.h:267-300);
+  * gather_objects / data_parallel_fields -- bench.py's N > 1 line: every rank's own ms/step,
+                           its exposed all-reduce wait and the bytes all-reduced per step, so a
+                           scaling run explains itself (weak-scaling loss vs exposed exchange).
 torch.distributed is plumbing only; the product math never goes through it.
 """
 from __future__ import annotations
@@ -52,3 +55,36 @@ def max_over_ranks(x: float) -> float:
     t = torch.tensor([float(x)], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def gather_objects(obj) -> list:
+    """Every rank's `obj` (a small picklable dict), in rank order, on every rank (gloo)."""
+    import torch.distributed as dist
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def data_parallel_fields(per_rank: Sequence[dict], grad_bytes: int, buckets: int | None) -> dict:
+    """The N > 1 fields of bench.py's line from every rank's own measurements.
+
+    per_rank[r] = {"ms_per_step": the rank's own timed-loop ms/step (before the max over ranks),
+                   "allreduce_ms": the rank's exposed all-reduce wait per step (the learner's
+                   "allreduce" phase: the compute stream waiting for buckets still in flight
+                   after the backward, HIP events over the profiled steps)}.
+    grad_bytes: the flat fp32 gradient all-reduced once per step (+ the 4-byte reject flag).
+    A ring all-reduce moves 2 (N - 1) / N of the buffer over each rank's links."""
+    n = len(per_rank)
+    ms = [float(d["ms_per_step"]) for d in per_rank]
+    ar = [float(d["allreduce_ms"]) for d in per_rank]
+    payload = int(grad_bytes) + 4
+    return {
+        "ranks": n,
+        "allreduce_bytes_per_step": payload,
+        "allreduce_ring_bytes_per_rank_per_step": int(round(2 * (n - 1) / n * payload)) if n else 0,
+        "allreduce_buckets_per_step": buckets,
+        "exposed_allreduce_ms": {"max": round(max(ar), 5), "mean": round(sum(ar) / n, 5),
+                                 "per_rank": [round(x, 5) for x in ar]},
+        "rank_ms_per_step": {"max": round(max(ms), 4), "mean": round(sum(ms) / n, 4),
+                             "min": round(min(ms), 4), "per_rank": [round(x, 4) for x in ms]},
+    }

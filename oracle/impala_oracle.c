@@ -381,6 +381,89 @@ static void conv_wgrad(int N, int IH, int IC, int K, int S, int OC, const float*
     }
 }
 
+/* Checker for the full-depth weight-gradient test (tests/test_gpu_atari.py): fp64 sums of a
+ * strided VALID conv's weight gradient straight from the GPU's own stored operands, for the
+ * output channels cos[0..ncos):
+ *   out[ky][kx][c][j] = sum_{n,oy,ox} X[n][oy*S+ky][ox*S+kx][c] * dY[n][oy][ox][cos[j]]
+ * X: u8 (x_kind 0: raw frames, NHWC), bf16 NHWC (1), or bf16 in the stride-2 parity-plane order
+ * [iy&1][ix&1][iy>>1][ix>>1][c] (2: conv21's a1 image order); dY: bf16 NHWC. No input scale.
+ * Frames are split over the OpenMP threads; each thread's partial sums are added in thread
+ * order (deterministic for a fixed thread count). Same arithmetic as conv_wgrad above, on the
+ * stored bf16 values (no re-rounding needed: bf16 -> double is exact). */
+static inline double bf16_bits_f64(uint16_t u) {
+    union { uint32_t i; float f; } v;
+    v.i = (uint32_t)u << 16;
+    return (double)v.f;
+}
+
+int orc_conv_wgrad_f64(int N, int IH, int IC, int K, int S, int OC, const void* X, int x_kind,
+                       const uint16_t* dY, int ncos, const int* cos, double* out) {
+    if (N < 0 || IH < K || K < 1 || S < 1 || IC < 1 || OC < 1 || ncos < 1 || ncos > 64) return -1;
+    if (x_kind == 2 && (IH & 1)) return -1;
+    const int OH = (IH - K) / S + 1, KK = K * K * IC, HH = IH / 2;
+    const size_t per = (size_t)KK * ncos;
+    const int nt = orc_num_threads();
+    double* part = (double*)calloc((size_t)nt * per, sizeof(double));
+    if (!part) return -2;
+#pragma omp parallel num_threads(nt)
+    {
+        int tid = 0;
+#ifdef _OPENMP
+        tid = omp_get_thread_num();
+#endif
+        double* acc = part + (size_t)tid * per;
+        double dy[64];
+        double* xs = (double*)malloc(sizeof(double) * (size_t)KK);
+#pragma omp for schedule(static)
+        for (int n = 0; n < N; ++n) {
+            for (int oy = 0; oy < OH; ++oy)
+                for (int ox = 0; ox < OH; ++ox) {
+                    const uint16_t* d = dY + (((size_t)n * OH + oy) * OH + ox) * OC;
+                    int any = 0;
+                    for (int j = 0; j < ncos; ++j) {
+                        dy[j] = bf16_bits_f64(d[cos[j]]);
+                        any |= dy[j] != 0.0;
+                    }
+                    if (!any) continue;
+                    for (int ky = 0; ky < K; ++ky)
+                        for (int kx = 0; kx < K; ++kx) {
+                            const int iy = oy * S + ky, ix = ox * S + kx;
+                            for (int c = 0; c < IC; ++c) {
+                                size_t e;
+                                if (x_kind == 2)
+                                    e = ((((size_t)n * 4 + (iy & 1) * 2 + (ix & 1)) * HH + (iy >> 1)) * HH + (ix >> 1)) * IC + c;
+                                else
+                                    e = (((size_t)n * IH + iy) * IH + ix) * IC + c;
+                                xs[(ky * K + kx) * IC + c] = x_kind == 0 ? (double)((const uint8_t*)X)[e]
+                                                                         : bf16_bits_f64(((const uint16_t*)X)[e]);
+                            }
+                        }
+                    if (ncos == 4) {  /* the test's case: a fixed-width inner loop the compiler vectorises */
+                        for (int kk = 0; kk < KK; ++kk) {
+                            const double x = xs[kk];
+                            double* a = acc + (size_t)kk * 4;
+                            for (int j = 0; j < 4; ++j) a[j] += x * dy[j];
+                        }
+                    } else {
+                        for (int kk = 0; kk < KK; ++kk) {
+                            const double x = xs[kk];
+                            double* a = acc + (size_t)kk * ncos;
+                            for (int j = 0; j < ncos; ++j) a[j] += x * dy[j];
+                        }
+                    }
+                }
+        }
+        free(xs);
+    }
+    for (size_t i = 0; i < per; ++i) {
+        double s = 0.0;
+        for (int t = 0; t < nt; ++t) s += part[(size_t)t * per + i];
+        out[i] = s;
+    }
+    free(part);
+    return 0;
+}
+
 typedef struct orc_atari_acts {
     float* x0;  /* N*84*84*4 frames as float (unscaled integers)          */
     float* a1;  /* N*20*20*32 */

@@ -65,6 +65,8 @@ def lib():
         L.orc_philox4.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, P]
         L.orc_synth_batch.argtypes = [C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                       C.c_int, C.c_float, P, P, P, P, P, P]
+        L.orc_conv_wgrad_f64.argtypes = [C.c_int] * 6 + [P, C.c_int, P, C.c_int, P, P]
+        L.orc_conv_wgrad_f64.restype = C.c_int
         L.orc_bf16_round.argtypes = [C.c_float]
         L.orc_bf16_round.restype = C.c_float
         L.orc_num_threads.restype = C.c_int
@@ -209,6 +211,22 @@ def synth_batch(seed, T, B, A=18, D=128, B_glob=None, b_off=0, gamma=0.99,
     lib().orc_synth_batch(seed, T, B, B_glob, b_off, A, D, gamma, _p(o), _p(mu), _p(act),
                           _p(rew), _p(disc), _p(fr))
     return dict(obs=o, frames=fr, mu=mu, actions=act, rewards=rew, discounts=disc)
+
+
+def conv_wgrad_f64(X, dY, N, IH, IC, K, S, OC, cos, x_kind):
+    """fp64 weight gradient of a strided VALID conv for output channels `cos` from stored operands
+    (X: uint8 frames (x_kind 0), bf16 bits NHWC (1) or in the parity-plane order (2); dY: bf16
+    bits NHWC) -> (K, K, IC, len(cos)), unscaled. Checker for the full-depth gradient test."""
+    X = np.ascontiguousarray(X)
+    dY = np.ascontiguousarray(dY, np.uint16)
+    assert X.dtype == (np.uint8 if x_kind == 0 else np.uint16) and X.size == N * IH * IH * IC
+    OH = (IH - K) // S + 1
+    assert dY.size == N * OH * OH * OC
+    c = np.ascontiguousarray(cos, np.int32)
+    out = np.zeros((K, K, IC, c.size), np.float64)
+    rc = lib().orc_conv_wgrad_f64(N, IH, IC, K, S, OC, _p(X), x_kind, _p(dY), c.size, _p(c), _p(out))
+    assert rc == 0, rc
+    return out
 
 
 def bf16_round(x):

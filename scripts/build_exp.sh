@@ -12,8 +12,8 @@ mkdir -p build/ab
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Iinclude -Ifreeimpala_amd/csrc \
   -Wno-unused-result -Wno-unused-value -munsafe-fp-atomics "$@" -x hip -c "$SRC" -o build/ab/x_$n.o
 objs=""
-for o in farmer.hip vtrace.hip gemm_f32.hip misc.hip atari.hip atari_fr.hip fc_gemm.hip fc_blaslt.cpp learner.cpp; do
+for o in farmer.hip vtrace.hip gemm_f32.hip misc.hip atari.hip atari_fr.hip fc_gemm.hip learner.cpp; do
   if [ "$o" = "$base" ]; then objs="$objs build/ab/x_$n.o"; else objs="$objs build/obj/$o.o"; fi
 done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o build/ab/lib_$n.so $objs \
-  -L/opt/rocm/lib -lrccl -lhipblaslt -Wl,-rpath,/opt/rocm/lib
+  -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib

@@ -9,4 +9,4 @@ mkdir -p build/exp
   -Wno-unused-result -Wno-unused-value "$@" -c freeimpala_amd/csrc/vtrace.hip -o build/exp/vt_$n.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o build/exp/libvt_$n.so build/exp/vt_$n.o \
   build/obj/gemm_f32.hip.o build/obj/misc.hip.o build/obj/atari.hip.o build/obj/atari_fr.hip.o \
-  build/obj/fc_blaslt.cpp.o build/obj/learner.cpp.o -L/opt/rocm/lib -lrccl -lhipblaslt -Wl,-rpath,/opt/rocm/lib
+  build/obj/fc_gemm.hip.o build/obj/farmer.hip.o build/obj/learner.cpp.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib

@@ -8,8 +8,6 @@
 #define FC_DG_CFG 224, 256, 1, 8, 64, 2, 1 | 2
 #define FC_WG_CFG 256, 224, 4, 2, 64, 2
 #include "../freeimpala_amd/csrc/fc_gemm.hip"
-#include "../freeimpala_amd/csrc/fc_blaslt.h"
-#include "fc_variants.hip"
 
 #include <cstdio>
 #include <algorithm>
@@ -76,30 +74,11 @@ int main(int argc, char** argv) {
     };
 #define FWDV(nm, ...) add("fwd  " nm, 0, [&](hipStream_t st, int k) { return fc_fwd_impl<__VA_ARGS__>(a3, wT, bias, h[k], R, st); }, h[0], h[1], (size_t)R * FCO * 2)
 #define DGV(nm, ...) add("dgrd " nm, 1, [&](hipStream_t st, int k) { return fc_dgrad_impl<__VA_ARGS__>(dh, w, da3[k], R, st); }, da3[0], da3[1], (size_t)R * FCK * 2)
-#define FWSV(nm, ...) add("fwd  " nm, 0, [&](hipStream_t st, int k) { return fc_fwd_ws_impl<__VA_ARGS__>(a3, wT, bias, h[k], R, st); }, h[0], h[1], (size_t)R * FCO * 2)
-#define DGSV(nm, ...) add("dgrd " nm, 1, [&](hipStream_t st, int k) { return fc_dgrad_ws_impl<__VA_ARGS__>(dh, w, da3[k], R, st); }, da3[0], da3[1], (size_t)R * FCK * 2)
 #define WGV(nm, S, ...) add("wgrd " nm, 2, [&](hipStream_t st, int k) { return fc_wgrad_impl<__VA_ARGS__>(a3, dh, slab, dw[k], R, st, S); }, dw[0], dw[1], (size_t)FCK * FCO * 4)
     // the shipped configurations first (fc_gemm.hip FC_*_CFG), then alternatives
     FWDV("256x256 w4x2 bk64 ns2 ntY midbar", 256, 256, 4, 2, 64, 2, 8 | 4096);
-    FWDV("256x256 w4x2 bk64 ns2 prio iss@frag", 256, 256, 4, 2, 64, 2, 1 | 16);
-    FWSV("ws 256x128 c2x2 l4 ntY", 256, 128, 2, 2, 4, 8);
-    add("fwd  4 waves, hand-placed asm half-steps", 0, [&](hipStream_t st, int k) { return fc_fwd_asm_impl(a3, wT, bias, h[k], R, st); }, h[0], h[1], (size_t)R * FCO * 2);
-    add("fwd  asm, k-half-split ring", 0, [&](hipStream_t st, int k) { return fc_fwd_asm2_impl(a3, wT, bias, h[k], R, st); }, h[0], h[1], (size_t)R * FCO * 2);
-    add("fwd  asm, one W half per XCD", 0, [&](hipStream_t st, int k) { return fc_fwd_asm_impl<2>(a3, wT, bias, h[k], R, st); }, h[0], h[1], (size_t)R * FCO * 2);
-    add("fwd  asm, no vmcnt wait (timing only)", 0, [&](hipStream_t st, int k) { return fc_fwd_asm_impl<1>(a3, wT, bias, h[k], R, st); }, h[0], h[1], (size_t)R * FCO * 2);
-    add("fwd  midbar ntY, one DMA asm block per step", 0, [&](hipStream_t st, int k) { return fc_fwd2_impl(a3, wT, bias, h[k], R, st); }, h[0], h[1], (size_t)R * FCO * 2);
     DGV("224x256 w1x8 bk64 ns2 prio ntst", 224, 256, 1, 8, 64, 2, 1 | 2);
-    DGSV("ws 224x128 c2x2 l4 ntst lprio", 224, 128, 2, 2, 4, 3);
     WGV("256x224 w4x2 bk64 ns2", 9, 256, 224, 4, 2, 64, 2);
-    // hipBLASLt (the default fwd / dgrad today), own output buffers: not bit-comparable
-    __bf16 *hb, *db;
-    CK(hipMalloc(&hb, (size_t)R * FCO * 2));
-    CK(hipMalloc(&db, (size_t)R * FCK * 2));
-    FcBlasLt* F = std::getenv("FCB_NO_BLASLT") ? nullptr : fc_blaslt_create(R, a3, w, dh, hb, db, s);
-    if (F) {
-        add("fwd  hipBLASLt", 3, [&](hipStream_t st, int) { return fc_blaslt_forward(F, a3, w, bias, hb, st); }, hb, hb, 0);
-        add("dgrd hipBLASLt", 4, [&](hipStream_t st, int) { return fc_blaslt_dgrad(F, dh, w, db, st); }, db, db, 0);
-    }
     std::vector<std::vector<float>> ms(vs.size());
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));

@@ -8,7 +8,12 @@ ROOT=$(pwd)
 OUT=$ROOT/gpurun_out
 TAG=${1:-r03}
 mkdir -p "$OUT"
-timeout -k 10 600 python -u -m pytest tests -v -m gpu -x --timeout 120 --timeout-method thread > "$OUT/pytest_gpu_$TAG.log" 2>&1
+# long silent steps (the full-size fp64 gradient check, the whole-step CPU baseline): a heartbeat
+# file under gpurun_out shows the call is alive
+( while sleep 30; do date +%T >> "$OUT/heartbeat_$TAG.txt"; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
+timeout -k 10 900 python -u -m pytest tests -v -m gpu -x --timeout 120 --timeout-method thread > "$OUT/pytest_gpu_$TAG.log" 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 "$OUT/pytest_gpu_$TAG.log"; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke_$TAG.txt" 2>&1
 rc=$?; echo "smoke rc=$rc"; tail -2 "$OUT/smoke_$TAG.txt"; [ $rc -ne 0 ] && exit $rc

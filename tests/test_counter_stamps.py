@@ -55,7 +55,7 @@ def test_bench_refuses_counters_of_another_shape(tmp_path, monkeypatch):
 
 
 def test_bench_refuses_counters_taken_under_other_switches(tmp_path, monkeypatch):
-    """the same sources run different kernels under FI_* switches (e.g. FI_FC_OWN,
+    """the same sources run different kernels under FI_* switches (e.g.
     FI_BWD_UNFUSED): a pass stamped under one setting is not attached to a line timed under
     another."""
     import bench

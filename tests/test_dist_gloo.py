@@ -95,3 +95,42 @@ def test_split_entries_and_shards():
     assert launch.shard_columns(3, 8, 4096) == (3 * 4096, 4096)
     with pytest.raises(ValueError):
         launch.shard_columns(8, 8, 4096)
+
+
+def _dp_fields_worker(rank, world, port, out_dir):
+    """bench.py's N > 1 reporting as it runs under torch.distributed.run (FI_BENCH_NO_COMM
+    rehearsal on CPU): each rank contributes its own ms/step and exposed all-reduce wait, every
+    rank gathers all of them and builds the line's data_parallel object."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import json
+    import torch.distributed as dist
+    from freeimpala_amd import launch
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        own = {"ms_per_step": 24.0 + rank, "allreduce_ms": 0.1 * (rank + 1)}
+        per = launch.gather_objects(own)
+        dp = launch.data_parallel_fields(per, grad_bytes=4 * 1693875, buckets=3)
+        with open(os.path.join(out_dir, f"dp{rank}.json"), "w") as fh:
+            json.dump(dp, fh)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_data_parallel_fields_world2(tmp_path):
+    """bench.py's N > 1 line carries the bytes all-reduced per step, the exposed
+    all-reduce wait per rank (max / mean) and every rank's own ms/step, gathered over gloo."""
+    import json
+    import torch.multiprocessing as mp
+    world = 2
+    mp.start_processes(_dp_fields_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    dps = [json.load(open(tmp_path / f"dp{r}.json")) for r in range(world)]
+    assert dps[0] == dps[1]  # every rank holds the same gathered view
+    dp = dps[0]
+    assert dp["ranks"] == 2
+    assert dp["allreduce_bytes_per_step"] == 4 * 1693875 + 4
+    assert dp["allreduce_ring_bytes_per_rank_per_step"] == 4 * 1693875 + 4  # 2 (N-1)/N = 1 at N = 2
+    assert dp["allreduce_buckets_per_step"] == 3
+    assert dp["rank_ms_per_step"]["per_rank"] == [24.0, 25.0] and dp["rank_ms_per_step"]["max"] == 25.0
+    assert dp["exposed_allreduce_ms"] == {"max": 0.2, "mean": 0.15, "per_rank": [0.1, 0.2]}

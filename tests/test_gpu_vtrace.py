@@ -82,17 +82,39 @@ def test_vtrace_golden(path):
     compare(out, {k: z[k] for k in ("vs", "pg_adv", "dlogits", "dvalue", "losses")})
 
 
+def str_shape_ok(T, A):
+    """variant 4's limits (vtrace.hip str_supported): T <= 127, T * A <= 2048 dlogits pieces, the
+    two whole-sequence slots within 160 KB of LDS."""
+    lds = 2 * 1024 * (2 * -(-T * 16 * A // 1024) + 3 * -(-T * 16 // 1024) + -(-(T + 1) * 16 // 1024)) + 256
+    return T <= 127 and T * A <= 2048 and lds <= 160 * 1024
+
+
 @pytest.mark.parametrize("T,B,A", [(1, 16, 18), (16, 16, 18), (17, 32, 18), (33, 48, 4),
                                    (100, 64, 2), (100, 32, 20), (50, 16, 6), (3, 16, 18),
                                    (100, 256, 18), (128, 64, 18), (127, 16, 18), (65, 24, 18)])
 @pytest.mark.parametrize("variant", [1, 2, 3, 4])
 def test_vtrace_kernels_vs_oracle(orc, T, B, A, variant):
-    if variant == 4 and T > 127 or variant == 4 and 2 * 1024 * (2 * -(-T * 16 * A // 1024) + 3 * -(-T * 16 // 1024) + -(-(T + 1) * 16 // 1024)) + 256 > 160 * 1024:
-        pytest.skip("the streaming kernel holds a group's whole sequence in LDS (T <= 124 at A = 18)")
+    if variant == 4 and not str_shape_ok(T, A):
+        pytest.skip("the streaming kernel holds a group's whole sequence in LDS and stores at most "
+                    "2,048 dlogits pieces (T <= 113 at A = 18)")
     case = rand_case(T * 1000 + B + A, T, B, A)
     ref = orc.vtrace_loss(*case)
     out = run_vtrace(*case, variant=variant)
     compare(out, ref)
+
+
+@pytest.mark.parametrize("T,A", [(113, 18), (120, 18), (102, 20), (110, 20)])
+def test_vtrace_streaming_kernel_edge_of_its_store_rounds(orc, T, A):
+    """variant 4 stores the dlogits tile in 4 rounds of 512 pieces, i.e. at most 2,048
+    = T * A pieces. At the edge (T * A <= 2048) it must match the oracle; past it (the LDS would
+    still fit) it must refuse loudly instead of leaving the rows past the last round unwritten."""
+    from freeimpala_amd._abi import FiError
+    case = rand_case(T * 31 + A, T, 8, A)
+    if T * A <= 2048:
+        compare(run_vtrace(*case, variant=4), orc.vtrace_loss(*case))
+    else:
+        with pytest.raises(FiError, match="T\\*A<=2048"):
+            run_vtrace(*case, variant=4)
 
 
 @pytest.mark.parametrize("T,B,A", [(7, 13, 18), (5, 40, 5), (100, 100, 33)])

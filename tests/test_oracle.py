@@ -131,3 +131,35 @@ def test_synth_shard_independent_of_gpu_count(orc):
     assert set(np.unique(full["rewards"]).tolist()) <= {-1.0, 0.0, 1.0}
     o = orc.synth_batch(7, T=63, B=64, A=18, D=32)["obs"]
     assert abs(o.mean()) < 0.02 and abs(o.std() - 1.0) < 0.02
+
+
+def _bf16_bits(a, rs=None):
+    return (np.asarray(a, np.float32).view(np.uint32) >> 16).astype(np.uint16)
+
+
+def test_conv_wgrad_f64_checker_matches_direct_sums(orc):
+    """The full-depth gradient test's fp64 checker (orc_conv_wgrad_f64) against direct numpy sums:
+    conv1 on u8 frames, conv2 on a1 in NHWC and in conv21's parity-plane order."""
+    rs = np.random.RandomState(4)
+    N = 5
+    fr = rs.randint(0, 256, (N, 84, 84, 4)).astype(np.uint8)
+    d1 = _bf16_bits(rs.randn(N, 20, 20, 32))
+    cos = [0, 9, 31]
+    got = orc.conv_wgrad_f64(fr, d1, N, 84, 4, 8, 4, 32, cos, x_kind=0)
+    df = (d1.astype(np.uint32) << 16).view(np.float32).astype(np.float64)[..., cos]
+    for ky, kx in [(0, 0), (3, 7), (7, 7)]:
+        ref = np.einsum("nyxc,nyxo->co", fr[:, ky:ky + 77:4, kx:kx + 77:4].astype(np.float64), df)
+        np.testing.assert_allclose(got[ky, kx], ref, rtol=1e-12)
+    a1 = _bf16_bits(rs.randn(N, 20, 20, 32))
+    d2 = _bf16_bits(rs.randn(N, 9, 9, 64))
+    planar = a1.reshape(N, 10, 2, 10, 2, 32).transpose(0, 2, 4, 1, 3, 5).copy()  # [iy&1][ix&1][iy>>1][ix>>1]
+    c2 = [1, 63]
+    g_nhwc = orc.conv_wgrad_f64(a1, d2, N, 20, 32, 4, 2, 64, c2, x_kind=1)
+    g_plan = orc.conv_wgrad_f64(planar, d2, N, 20, 32, 4, 2, 64, c2, x_kind=2)
+    np.testing.assert_array_equal(g_nhwc, g_plan)
+    af = (a1.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
+    d2f = (d2.astype(np.uint32) << 16).view(np.float32).astype(np.float64)[..., c2]
+    for ky in range(4):
+        for kx in range(4):
+            ref = np.einsum("nyxc,nyxo->co", af[:, ky:ky + 17:2, kx:kx + 17:2], d2f)
+            np.testing.assert_allclose(g_nhwc[ky, kx], ref, rtol=1e-12)
