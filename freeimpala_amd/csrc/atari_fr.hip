@@ -31,6 +31,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
 
@@ -58,6 +59,60 @@ constexpr int OUT = 400 * 32 * 2;                   // 25,600 B output / dY tile
 #ifndef FI_C21_PKMASK
 #define FI_C21_PKMASK 1
 #endif
+// The weight gradients' 32x32x16 MFMA. FI_EXP_MFMA16 (timing only, WRONG results): the same
+// flops as two 16x16x32 MFMAs on the same operand registers into two quarters of the
+// accumulator, to price the MFMA shape's clock under the power limit (MI355X_MICROARCH.md:
+// 16x16x32 loops hold a higher clock than 32x32x16 at equal cycles per FLOP).
+#ifndef FI_EXP_MFMA16
+#define FI_EXP_MFMA16 0
+#endif
+__device__ __forceinline__ f32x16 mfma_wg(const bf16x8& a, const bf16x8& b, f32x16 acc) {
+#if FI_EXP_MFMA16
+    f32x4 q0 = __builtin_shufflevector(acc, acc, 0, 1, 2, 3), q1 = __builtin_shufflevector(acc, acc, 4, 5, 6, 7);
+    q0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, q0, 0, 0, 0);
+    q1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, a, q1, 0, 0, 0);
+    const f32x4 r2 = __builtin_shufflevector(acc, acc, 8, 9, 10, 11), r3 = __builtin_shufflevector(acc, acc, 12, 13, 14, 15);
+    const f32x8 lo = __builtin_shufflevector(q0, q1, 0, 1, 2, 3, 4, 5, 6, 7);
+    const f32x8 hi = __builtin_shufflevector(r2, r3, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+#else
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+#endif
+}
+
+// Blocked fp32 accumulation of the persistent weight gradients. A workgroup walks ~1,616 frames
+// at the bench size; one fp32 accumulator chain over all of them (conv1's weight gradient: 25
+// MFMA steps per frame, ~40k accumulate roundings per element) measured 1.8e-5 relative L2
+// against fp64 (tests/test_gpu_atari.py, full size) -- over SURVEY.md's 1e-5 bar. So:
+//  * conv2's weight gradient (128 accumulators per wave, no registers to spare) is written as
+//    WG_SEGS partial slabs per workgroup, one per contiguous segment of its frames (segment k
+//    ends after frame seg_last(k)); the slabs are summed by reduce_slabs in a fixed order;
+//  * conv1's (32 accumulators) is summed into a second register set every C1_GROUP frames.
+constexpr int WG_SEGS = 4;
+constexpr int C1_GROUP = 8;
+__device__ __forceinline__ int seg_last(int k, int nmine) { return ((k + 1) * nmine) / WG_SEGS - 1; }
+
+// one conv2 weight-gradient slab [512][64] from a wave's accumulators (kernel row wr), zeroing
+// them; with `drain` the stores (and every other outstanding VMEM op of the wave) complete
+// before the frame loop's counted vmcnt waits resume
+// (buffer stores: one per-lane offset register, the wave-uniform rest in soffset -- 128 flat
+// stores with 64-bit addresses each spilled the frame loop's registers)
+__device__ __forceinline__ void c2w_flush(f32x16 (&accw)[4][2], float* out, int wr, int h, int col, bool drain) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(out + (size_t)128 * wr * 64, 0, 128 * 64 * 4, 0x00020000);
+    const int vo = fi_opaque((4 * h * 64 + col) * 4);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {
+#pragma unroll
+            for (int rr = 0; rr < 16; ++rr)
+                __builtin_amdgcn_raw_buffer_store_b32(accw[t][ct][rr], r, vo,
+                                                      ((32 * t + (rr & 3) + 8 * (rr >> 2)) * 64 + 32 * ct) * 4, 0);
+            accw[t][ct] = f32x16{};
+        }
+    if (drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // sum of a fragment's 8 bf16 values into acc: 4 v_dot2c_f32_bf16 against (1, 1) instead of 8
 // conversions + 8 adds (the weight-gradient waves' bias column sums of dY)
 __device__ __forceinline__ float sum8_bf16(const bf16x8& v, float acc) {
@@ -333,7 +388,7 @@ __global__ __launch_bounds__(512, 2) void conv1_wgrad_fr(const uint8_t* __restri
             }
 #pragma unroll
             for (int kt = 0; kt < 4; ++kt)
-                acc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[1 + kt], cur[0], acc[kt], 0, 0, 0);
+                acc[kt] = mfma_wg(cur[1 + kt], cur[0], acc[kt]);
         };
         bf16x8 fb[2][5];
         load(0, fb[0]);
@@ -999,7 +1054,7 @@ __global__ __launch_bounds__(512, 2) void conv2_bwd_fr(const __bf16* __restrict_
                                                        const __bf16* __restrict__ da2,
                                                        const __bf16* __restrict__ w2d,  // [4][32][256]
                                                        __bf16* __restrict__ da1,
-                                                       float* __restrict__ slab,     // [grid][512][64]
+                                                       float* __restrict__ slab,     // [grid][WG_SEGS][512][64]
                                                        float* __restrict__ cs_slab,  // [grid][64]
                                                        int nframes) {
     __shared__ __attribute__((aligned(16))) char smem[c2::RING * c2::SLOT + c2::SLOT / 16 * 4];
@@ -1022,6 +1077,9 @@ __global__ __launch_bounds__(512, 2) void conv2_bwd_fr(const __bf16* __restrict_
 #pragma unroll
         for (int t = 0; t < 4; ++t) { accw[t][0] = f32x16{}; accw[t][1] = f32x16{}; }
         float bsum0 = 0.f, bsum1 = 0.f;
+        const int nmine = nframes > (int)blockIdx.x ? (nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+        float* const out = slab + (size_t)blockIdx.x * WG_SEGS * 512 * 64;
+        int it = 0, seg = 0;
         c2_frames(ctx, smem, 0, [&](const char* X, int) {
             // software pipeline: the 6 fragments of step ms+1 (12 transposed reads) are issued
             // between the 8 MFMAs of step ms; sched_group_barrier pins that interleave
@@ -1048,8 +1106,8 @@ __global__ __launch_bounds__(512, 2) void conv2_bwd_fr(const __bf16* __restrict_
                 bsum1 = sum8_bf16(cur[1], bsum1);
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
-                    accw[t][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[2 + t], cur[0], accw[t][0], 0, 0, 0);
-                    accw[t][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[2 + t], cur[1], accw[t][1], 0, 0, 0);
+                    accw[t][0] = mfma_wg(cur[2 + t], cur[0], accw[t][0]);
+                    accw[t][1] = mfma_wg(cur[2 + t], cur[1], accw[t][1]);
                 }
 #pragma unroll
                 for (int k = 0; k < 8; ++k) {
@@ -1060,17 +1118,13 @@ __global__ __launch_bounds__(512, 2) void conv2_bwd_fr(const __bf16* __restrict_
                     }
                 }
             }
+            if (seg < WG_SEGS - 1 && it == seg_last(seg, nmine)) {  // as conv21_bwd_fr (bit-identical)
+                c2w_flush(accw, out + (size_t)seg * 512 * 64, wr, h, col, true);
+                ++seg;
+            }
+            ++it;
         });
-        float* out = slab + (size_t)blockIdx.x * 512 * 64;
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-            for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int k = 128 * wr + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    out[k * 64 + 32 * ct + col] = accw[t][ct][r];
-                }
+        for (; seg < WG_SEGS; ++seg) c2w_flush(accw, out + (size_t)seg * 512 * 64, wr, h, col, false);
         // lanes l and l+32 hold the same co (16*(g&1) + (l&15)), other m half; cs_slab has the
         // [grid][2][64] layout of conv21_bwd_fr's (row 1 zero), unless conv3_bwd fills it (FI_C2B_C3)
         if (!FI_C2B_C3 && wr == 0) {
@@ -1211,7 +1265,7 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                                                         const __bf16* __restrict__ w2d,  // [4][32][256]
                                                         const uint8_t* __restrict__ frames,
                                                         __bf16* __restrict__ da1_out,  // optional (parity checks)
-                                                        float* __restrict__ slab2,     // [grid][512][64]
+                                                        float* __restrict__ slab2,     // [grid][WG_SEGS][512][64]
                                                         float* __restrict__ cs2,       // [grid][2][64] (unless FI_C2B_C3)
                                                         float* __restrict__ slab1,     // [grid][256][32]
                                                         float* __restrict__ cs1,       // [grid][4 waves][32]
@@ -1255,7 +1309,8 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
     auto dsw = [](int m, int c) { return 64 * m + 16 * (c ^ ((m >> 1) & 3)); };
     const int dc = 2 * (g & 1) + (p4 >> 1);
     const int db0 = dsw(8 * (g >> 1) + q, dc) + 8 * (p4 & 1), db1 = dsw(8 * (g >> 1) + q + 4, dc) + 8 * (p4 & 1);
-    f32x16 acc1[2] = {};
+    f32x16 acc1[2] = {};  // this group's C1_GROUP frames (MFMA accumulators)
+    f32x16 sum1[2] = {};  // the workgroup's frames so far (blocked accumulation, WG_SEGS above)
     // conv1's bias gradient = column sums of da1: the B fragment of m-step ms holds 8 pixels of
     // channel lane & 31, so wave 4 + wr sums the fragments of m-steps ms = wr (mod 4) beside its
     // MFMAs (4 v_dot2 in a 64-cycle MFMA pair) instead of 16 VALU per tile in the phase-1 epilogue
@@ -1292,7 +1347,7 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
             const bf16x8* cur = fb[ms % (PD + 1)];
 #pragma unroll
             for (int kt = 0; kt < 2; ++kt)
-                acc1[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[1 + kt], cur[0], acc1[kt], 0, 0, 0);
+                acc1[kt] = mfma_wg(cur[1 + kt], cur[0], acc1[kt]);
             if constexpr (FI_C1B_PH2) {
                 if ((ms & 3) == decltype(wrc)::value) bsum1 = sum8_bf16(cur[0], bsum1);
             }
@@ -1346,6 +1401,8 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
 #pragma unroll
         for (int t = 0; t < 4; ++t) { accw[t][0] = f32x16{}; accw[t][1] = f32x16{}; }
         float bsum0 = 0.f, bsum1_ = 0.f;
+        float* const out2 = slab2 + (size_t)blockIdx.x * WG_SEGS * 512 * 64;
+        int seg = 0;
         int issued = 0, m_dy = 0;
         if (nmine > 0) issued += issue_ax(0, 0);
         if (nmine > 1) issued += issue_ax(1, 1);
@@ -1384,8 +1441,8 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                     }
 #pragma unroll
                     for (int t = 0; t < 4; ++t) {
-                        accw[t][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[2 + t], cur[0], accw[t][0], 0, 0, 0);
-                        accw[t][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[2 + t], cur[1], accw[t][1], 0, 0, 0);
+                        accw[t][0] = mfma_wg(cur[2 + t], cur[0], accw[t][0]);
+                        accw[t][1] = mfma_wg(cur[2 + t], cur[1], accw[t][1]);
                     }
 #pragma unroll
                     for (int k = 0; k < 8; ++k) {
@@ -1396,6 +1453,11 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                         }
                     }
                 }
+            }
+            // conv2 weight-gradient segment done: its partial slab out (a drain once per segment)
+            if (seg < WG_SEGS - 1 && it == seg_last(seg, nmine)) {
+                c2w_flush(accw, out2 + (size_t)seg * 512 * 64, wr, h, col, true);
+                ++seg;
             }
 #pragma unroll
             for (int i = 0; i < c21::NRAW_A; ++i) {  // raw(it) -> bf16 pair-plane image (free since B1)
@@ -1422,16 +1484,7 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
             if (it + 2 < nmine) issued += issue_ax(it + 2, it & 1);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        float* out = slab2 + (size_t)blockIdx.x * 512 * 64;
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-            for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int k = 128 * wr + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    out[k * 64 + 32 * ct + col] = accw[t][ct][r];
-                }
+        for (; seg < WG_SEGS; ++seg) c2w_flush(accw, out2 + (size_t)seg * 512 * 64, wr, h, col, false);
         if constexpr (!FI_C2B_C3) {  // cs2[block][0][64] (row [1] zero: the layout conv3_bwd fills otherwise)
             if (wr == 0) {
                 const float o0 = __shfl_xor(bsum0, 32, 64), o1 = __shfl_xor(bsum1_, 32, 64);
@@ -1565,7 +1618,16 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                 case 2: conv1_wgrad(std::integral_constant<int, 2>{}); break;
                 default: conv1_wgrad(std::integral_constant<int, 3>{}); break;
             }
+            if ((it & (C1_GROUP - 1)) == C1_GROUP - 1) {
+#pragma unroll
+                for (int kt = 0; kt < 2; ++kt) {
+                    sum1[kt] += acc1[kt];
+                    acc1[kt] = f32x16{};
+                }
+            }
         }
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) sum1[kt] += acc1[kt];
         // conv1 bias partial of this wave: channel lane & 31, the two pixel halves of the B
         // fragments combined
         if constexpr (FI_C1B_PH2) {
@@ -1589,7 +1651,7 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
         for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
             for (int r = 0; r < 16; ++r)
-                out1[(32 * (2 * wr + kt) + (r & 3) + 8 * (r >> 2) + 4 * h) * 32 + col] = acc1[kt][r] * inv255;
+                out1[(32 * (2 * wr + kt) + (r & 3) + 8 * (r >> 2) + 4 * h) * 32 + col] = sum1[kt][r] * inv255;
     }
 }
 
@@ -1808,8 +1870,8 @@ __device__ __forceinline__ void c3_wgrad(const C3Ctx& ctx, char* smem, float* sl
             bsum1 = sum8_bf16(cur[1], bsum1);
 #pragma unroll
             for (int i = 0; i < NKT; ++i) {
-                accw[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[2 + i], cur[0], accw[i][0], 0, 0, 0);
-                accw[i][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[2 + i], cur[1], accw[i][1], 0, 0, 0);
+                accw[i][0] = mfma_wg(cur[2 + i], cur[0], accw[i][0]);
+                accw[i][1] = mfma_wg(cur[2 + i], cur[1], accw[i][1]);
             }
             // 2NKT MFMAs, 2NKT + 4 reads of the next step: pairs of reads between MFMAs
 #pragma unroll

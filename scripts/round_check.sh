@@ -13,6 +13,7 @@ mkdir -p "$OUT"
 ( while sleep 30; do date +%T >> "$OUT/heartbeat_$TAG.txt"; done ) &
 HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
+export FI_TEST_REPORT_DIR=$OUT
 timeout -k 10 900 python -u -m pytest tests -v -m gpu -x --timeout 120 --timeout-method thread > "$OUT/pytest_gpu_$TAG.log" 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 "$OUT/pytest_gpu_$TAG.log"; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke_$TAG.txt" 2>&1

@@ -361,6 +361,17 @@ def test_atari_full_size_sampled_forward_and_determinism(orc):
         L.close()
 
 
+def _report(name, obj):
+    """Measured errors as JSON under $FI_TEST_REPORT_DIR (scripts/round_check.sh points it at
+    gpurun_out/), whether the test passes or not."""
+    import json
+    import os
+    d = os.environ.get("FI_TEST_REPORT_DIR")
+    if d and os.path.isdir(d):
+        with open(os.path.join(d, name + ".json"), "w") as fh:
+            json.dump(obj, fh, indent=1)
+
+
 def _bf16_rows_f64(u16, r0, r1):
     """rows [r0, r1) of a bf16 (uint16) array as float64 (bf16 -> fp32 is exact)."""
     return bf16_to_f32(u16[r0:r1]).astype(np.float64)
@@ -412,6 +423,7 @@ def test_atari_full_size_gradient_vs_fp64(orc, monkeypatch):
         ref = np.asarray(ref, np.float64).ravel()
         errs[nm] = (float(np.linalg.norm(got - ref) / max(1e-30, np.linalg.norm(ref))),
                     float(np.abs(got - ref).max() / max(1e-30, np.abs(ref).max())))
+        _report("full_size_gradient_errors", errs)  # also when a later check fails
         rel(got, ref, nm, l2=l2, mx=mx)
 
     # conv1 / conv2 weight gradients (VERDICT r4 Missing #2): the sums conv21_bwd_fr keeps in
@@ -473,6 +485,7 @@ def test_atari_full_size_gradient_vs_fp64(orc, monkeypatch):
     check(f"c3W[..., {co}]", gs["c3W"].reshape(3, 3, 64, 64)[..., co], c3w, 1e-5, 1e-4)
     print("full-size gradient vs fp64 (rel L2, scaled max):",
           {k: (f"{a:.2e}", f"{b:.2e}") for k, (a, b) in errs.items()})
+    _report("full_size_gradient_errors", errs)
     for X in (L, twin):
         X.close()
 
