@@ -25,7 +25,7 @@ TAGS = {
         "conv21_bwd": ("conv21_bwd_fr", 1, 0), "conv12_fwd": ("conv12_fwd_fr", 1, 0),
         "conv3_bwd": ("conv3_bwd_fr", 1, 0), "conv3_fwd": ("conv_fwd_fr<3>", 1, 0),
         "vtrace": ("vtrace_lds_kernel", 1, 0), "fc_wgrad": ("fc_tn_kernel", 1, 0),
-        "fc_nt (own fwd/dgrad)": ("fc_nt_kernel", 1, 0), "fc (hipBLASLt)": ("Cijk_", 1, 0),
+        "fc_fwd": ("fcg::EpiFwd", 1, 0), "fc_dgrad": ("fcg::EpiDgrad", 1, 0),
         "heads_fwd": ("EpiHeads", 1, 0), "heads_dgrad": ("heads_dgrad", 1, 0),
         "heads_wgrad": ("heads_wgrad", 1, 0),
     },

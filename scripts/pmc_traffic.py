@@ -32,6 +32,8 @@ TAGS = {
         "conv3_bwd": ("conv3_bwd_fr", 1, 0),
         "conv21_bwd": ("conv21_bwd_fr", 1, 0),
         "fc_wgrad": ("fc_tn_kernel", 1, 0),
+        "fc_fwd": ("fcg::EpiFwd", 1, 0),
+        "fc_dgrad": ("fcg::EpiDgrad", 1, 0),
         "heads_dgrad": ("heads_dgrad", 1, 0),
         "heads_wgrad": ("heads_wgrad", 1, 0),
     },
