@@ -105,9 +105,11 @@ __device__ __forceinline__ void c2w_flush(f32x16 (&accw)[4][2], float* out, int 
 #pragma unroll
         for (int ct = 0; ct < 2; ++ct) {
 #pragma unroll
-            for (int rr = 0; rr < 16; ++rr)
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, accw[t][ct][rr]), r, vo,
+            for (int rr = 0; rr < 16; ++rr) {
+                const float v = accw[t][ct][rr];
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, vo,
                                                       ((32 * t + (rr & 3) + 8 * (rr >> 2)) * 64 + 32 * ct) * 4, 0);
+            }
             accw[t][ct] = f32x16{};
         }
     if (drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
