@@ -88,8 +88,14 @@ __device__ __forceinline__ f32x16 mfma_wg(const bf16x8& a, const bf16x8& b, f32x
 //    WG_SEGS partial slabs per workgroup, one per contiguous segment of its frames (segment k
 //    ends after frame seg_last(k)); the slabs are summed by reduce_slabs in a fixed order;
 //  * conv1's (32 accumulators) is summed into a second register set every C1_GROUP frames.
-constexpr int WG_SEGS = 4;
-constexpr int C1_GROUP = 8;
+#ifndef FI_WG_SEGS
+#define FI_WG_SEGS 4
+#endif
+#ifndef FI_C1_GROUP
+#define FI_C1_GROUP 8  // 0: one chain (A/B only)
+#endif
+constexpr int WG_SEGS = FI_WG_SEGS;
+constexpr int C1_GROUP = FI_C1_GROUP;
 __device__ __forceinline__ int seg_last(int k, int nmine) { return ((k + 1) * nmine) / WG_SEGS - 1; }
 
 // one conv2 weight-gradient slab [512][64] from a wave's accumulators (kernel row wr), zeroing
@@ -1620,11 +1626,13 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                 case 2: conv1_wgrad(std::integral_constant<int, 2>{}); break;
                 default: conv1_wgrad(std::integral_constant<int, 3>{}); break;
             }
-            if ((it & (C1_GROUP - 1)) == C1_GROUP - 1) {
+            if constexpr (C1_GROUP > 0) {
+                if ((it & (C1_GROUP - 1)) == C1_GROUP - 1) {
 #pragma unroll
-                for (int kt = 0; kt < 2; ++kt) {
-                    sum1[kt] += acc1[kt];
-                    acc1[kt] = f32x16{};
+                    for (int kt = 0; kt < 2; ++kt) {
+                        sum1[kt] += acc1[kt];
+                        acc1[kt] = f32x16{};
+                    }
                 }
             }
         }
