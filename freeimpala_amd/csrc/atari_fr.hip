@@ -83,20 +83,18 @@ __device__ __forceinline__ f32x16 mfma_wg(const bf16x8& a, const bf16x8& b, f32x
 // Blocked fp32 accumulation of the persistent weight gradients. A workgroup walks ~1,616 frames
 // at the bench size; one fp32 accumulator chain over all of them (conv1's weight gradient: 25
 // MFMA steps per frame, ~40k accumulate roundings per element) measured 1.8e-5 relative L2
-// against fp64 (tests/test_gpu_atari.py, full size) -- over SURVEY.md's 1e-5 bar. So:
-//  * conv2's weight gradient (128 accumulators per wave, no registers to spare) is written as
-//    WG_SEGS partial slabs per workgroup, one per contiguous segment of its frames (segment k
-//    ends after frame seg_last(k)); the slabs are summed by reduce_slabs in a fixed order;
-//  * conv1's (32 accumulators) is summed into a second register set every C1_GROUP frames.
-#ifndef FI_WG_SEGS
-#define FI_WG_SEGS 4
-#endif
-#ifndef FI_C1_GROUP
-#define FI_C1_GROUP 8  // 0: one chain (A/B only)
-#endif
-constexpr int WG_SEGS = FI_WG_SEGS;
-constexpr int C1_GROUP = FI_C1_GROUP;
-__device__ __forceinline__ int seg_last(int k, int nmine) { return ((k + 1) * nmine) / WG_SEGS - 1; }
+// against fp64 (tests/test_gpu_atari.py, full size) -- over SURVEY.md's 1e-5 bar. So conv21_bwd_fr
+// walks its frames in SEGS contiguous segments (segment k ends after frame seg_last(k)) and
+// writes partial slabs at segment ends, outside the frame loop: conv1's weight gradient one per
+// segment, conv2's one per C2_EVERY segments (its error is ~4x smaller per frame); reduce_slabs
+// sums them in a fixed order. (A second conv1 register set, or the flush as a branch inside the
+// frame loop, each cost conv21 0.14-0.17 ms: profiles/r05_blocked_accumulation_ab.txt.)
+constexpr int SEGS = 8;
+constexpr int C2_EVERY = 4;
+constexpr int C2_SEGS = SEGS / C2_EVERY;  // conv2 weight-gradient slabs per workgroup
+__device__ __forceinline__ int seg_last(int k, int nmine) { return ((k + 1) * nmine) / SEGS - 1; }
+// last frame of conv2 segment j (the end of segment C2_EVERY (j + 1) - 1)
+__device__ __forceinline__ int c2_seg_last(int j, int nmine) { return seg_last(C2_EVERY * (j + 1) - 1, nmine); }
 
 // one conv2 weight-gradient slab [512][64] from a wave's accumulators (kernel row wr), zeroing
 // them; with `drain` the stores (and every other outstanding VMEM op of the wave) complete
@@ -1062,7 +1060,7 @@ __global__ __launch_bounds__(512, 2) void conv2_bwd_fr(const __bf16* __restrict_
                                                        const __bf16* __restrict__ da2,
                                                        const __bf16* __restrict__ w2d,  // [4][32][256]
                                                        __bf16* __restrict__ da1,
-                                                       float* __restrict__ slab,     // [grid][WG_SEGS][512][64]
+                                                       float* __restrict__ slab,     // [grid][C2_SEGS][512][64]
                                                        float* __restrict__ cs_slab,  // [grid][64]
                                                        int nframes) {
     __shared__ __attribute__((aligned(16))) char smem[c2::RING * c2::SLOT + c2::SLOT / 16 * 4];
@@ -1086,8 +1084,11 @@ __global__ __launch_bounds__(512, 2) void conv2_bwd_fr(const __bf16* __restrict_
         for (int t = 0; t < 4; ++t) { accw[t][0] = f32x16{}; accw[t][1] = f32x16{}; }
         float bsum0 = 0.f, bsum1 = 0.f;
         const int nmine = nframes > (int)blockIdx.x ? (nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
-        float* const out = slab + (size_t)blockIdx.x * WG_SEGS * 512 * 64;
+        float* const out = slab + (size_t)blockIdx.x * C2_SEGS * 512 * 64;
         int it = 0, seg = 0;
+        // conv21_bwd_fr's conv2 slabs exactly: slab j holds frames (c2_seg_last(j - 1), c2_seg_last(j)],
+        // empty segments are zero slabs (bit-identical gradients, test_fused_conv21_...)
+        while (seg < C2_SEGS - 1 && c2_seg_last(seg, nmine) < 0) c2w_flush(accw, out + (size_t)seg++ * 512 * 64, wr, h, col, false);
         c2_frames(ctx, smem, 0, [&](const char* X, int) {
             // software pipeline: the 6 fragments of step ms+1 (12 transposed reads) are issued
             // between the 8 MFMAs of step ms; sched_group_barrier pins that interleave
@@ -1126,13 +1127,11 @@ __global__ __launch_bounds__(512, 2) void conv2_bwd_fr(const __bf16* __restrict_
                     }
                 }
             }
-            if (seg < WG_SEGS - 1 && it == seg_last(seg, nmine)) {  // as conv21_bwd_fr (bit-identical)
-                c2w_flush(accw, out + (size_t)seg * 512 * 64, wr, h, col, true);
-                ++seg;
-            }
+            while (seg < C2_SEGS - 1 && it == c2_seg_last(seg, nmine))
+                c2w_flush(accw, out + (size_t)seg++ * 512 * 64, wr, h, col, true);
             ++it;
         });
-        for (; seg < WG_SEGS; ++seg) c2w_flush(accw, out + (size_t)seg * 512 * 64, wr, h, col, false);
+        for (; seg < C2_SEGS; ++seg) c2w_flush(accw, out + (size_t)seg * 512 * 64, wr, h, col, false);
         // lanes l and l+32 hold the same co (16*(g&1) + (l&15)), other m half; cs_slab has the
         // [grid][2][64] layout of conv21_bwd_fr's (row 1 zero), unless conv3_bwd fills it (FI_C2B_C3)
         if (!FI_C2B_C3 && wr == 0) {
@@ -1273,9 +1272,9 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                                                         const __bf16* __restrict__ w2d,  // [4][32][256]
                                                         const uint8_t* __restrict__ frames,
                                                         __bf16* __restrict__ da1_out,  // optional (parity checks)
-                                                        float* __restrict__ slab2,     // [grid][WG_SEGS][512][64]
+                                                        float* __restrict__ slab2,     // [grid][C2_SEGS][512][64]
                                                         float* __restrict__ cs2,       // [grid][2][64] (unless FI_C2B_C3)
-                                                        float* __restrict__ slab1,     // [grid][256][32]
+                                                        float* __restrict__ slab1,     // [grid][SEGS][256][32]
                                                         float* __restrict__ cs1,       // [grid][4 waves][32]
                                                         int nframes, int a1_planar) {
     __shared__ __attribute__((aligned(16))) char smem[c21::LDS];
@@ -1317,8 +1316,7 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
     auto dsw = [](int m, int c) { return 64 * m + 16 * (c ^ ((m >> 1) & 3)); };
     const int dc = 2 * (g & 1) + (p4 >> 1);
     const int db0 = dsw(8 * (g >> 1) + q, dc) + 8 * (p4 & 1), db1 = dsw(8 * (g >> 1) + q + 4, dc) + 8 * (p4 & 1);
-    f32x16 acc1[2] = {};  // this group's C1_GROUP frames (MFMA accumulators)
-    f32x16 sum1[2] = {};  // the workgroup's frames so far (blocked accumulation, WG_SEGS above)
+    f32x16 acc1[2] = {};  // this segment's frames (blocked accumulation, SEGS above)
     // conv1's bias gradient = column sums of da1: the B fragment of m-step ms holds 8 pixels of
     // channel lane & 31, so wave 4 + wr sums the fragments of m-steps ms = wr (mod 4) beside its
     // MFMAs (4 v_dot2 in a 64-cycle MFMA pair) instead of 16 VALU per tile in the phase-1 epilogue
@@ -1409,8 +1407,7 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
 #pragma unroll
         for (int t = 0; t < 4; ++t) { accw[t][0] = f32x16{}; accw[t][1] = f32x16{}; }
         float bsum0 = 0.f, bsum1_ = 0.f;
-        float* const out2 = slab2 + (size_t)blockIdx.x * WG_SEGS * 512 * 64;
-        int seg = 0;
+        float* const out2 = slab2 + (size_t)blockIdx.x * C2_SEGS * 512 * 64;
         int issued = 0, m_dy = 0;
         if (nmine > 0) issued += issue_ax(0, 0);
         if (nmine > 1) issued += issue_ax(1, 1);
@@ -1420,7 +1417,9 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
             load_raw(0);
             issued += c21::NRAW_A;
         }
-        for (int it = 0; it < nmine; ++it) {
+        int it = 0;
+        for (int sg = 0; sg < SEGS; ++sg) {
+          for (const int stop = seg_last(sg, nmine) + 1; it < stop; ++it) {
             wait_vmcnt(issued - m_dy);  // own pieces of da2(it) landed (a1(it) is older)
             lds_barrier();  // B1: frame it's images in LDS; frame it-1's D and image consumed
             {
@@ -1462,11 +1461,6 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                     }
                 }
             }
-            // conv2 weight-gradient segment done: its partial slab out (a drain once per segment)
-            if (seg < WG_SEGS - 1 && it == seg_last(seg, nmine)) {
-                c2w_flush(accw, out2 + (size_t)seg * 512 * 64, wr, h, col, true);
-                ++seg;
-            }
 #pragma unroll
             for (int i = 0; i < c21::NRAW_A; ++i) {  // raw(it) -> bf16 pair-plane image (free since B1)
                 const int u = tid + 256 * i;
@@ -1490,9 +1484,10 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                 m_dy = issued;
             }
             if (it + 2 < nmine) issued += issue_ax(it + 2, it & 1);
+          }
+          // conv2 segment done: its partial slab out (the drain keeps the counted waits exact)
+          if ((sg + 1) % C2_EVERY == 0) c2w_flush(accw, out2 + (size_t)((sg + 1) / C2_EVERY - 1) * 512 * 64, wr, h, col, true);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        for (; seg < WG_SEGS; ++seg) c2w_flush(accw, out2 + (size_t)seg * 512 * 64, wr, h, col, false);
         if constexpr (!FI_C2B_C3) {  // cs2[block][0][64] (row [1] zero: the layout conv3_bwd fills otherwise)
             if (wr == 0) {
                 const float o0 = __shfl_xor(bsum0, 32, 64), o1 = __shfl_xor(bsum1_, 32, 64);
@@ -1533,7 +1528,9 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
         const int bd0 = 16 * (si + 128 * g + c2::zc(g));
         const int bd6 = 16 * (min(96 + si, 99) + 128 * g + c2::zc(g));
         float bs8[8] = {};  // !FI_C1B_PH2: conv1 bias partials, channels 8g + j of this lane's da1 pixels
-        for (int it = 0; it < nmine; ++it) {
+        int it = 0;
+        for (int sg = 0; sg < SEGS; ++sg) {
+          for (const int stop = seg_last(sg, nmine) + 1; it < stop; ++it) {
             const int f = frame_of(it);
             lds_barrier();  // B1
             {  // conv2 data gradient of class (ty, tx) -> D (and da1_out)
@@ -1626,18 +1623,23 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                 case 2: conv1_wgrad(std::integral_constant<int, 2>{}); break;
                 default: conv1_wgrad(std::integral_constant<int, 3>{}); break;
             }
-            if constexpr (C1_GROUP > 0) {
-                if ((it & (C1_GROUP - 1)) == C1_GROUP - 1) {
+          }
+          // conv1 segment done: its partial slab out, rows k = 32(2wr + kt) + (r&3) + 8(r>>2) +
+          // 4(lane>>5) (x 1/255). Plain stores: these waves issue no counted DMA
+          const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc(
+              slab1 + ((size_t)blockIdx.x * SEGS + sg) * 256 * 32 + 64 * wr * 32, 0, 64 * 32 * 4, 0x00020000);
+          const int vo1 = fi_opaque((4 * h * 32 + col) * 4);
 #pragma unroll
-                    for (int kt = 0; kt < 2; ++kt) {
-                        sum1[kt] += acc1[kt];
-                        acc1[kt] = f32x16{};
-                    }
-                }
-            }
+          for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+              for (int rr = 0; rr < 16; ++rr) {
+                  const float v = acc1[kt][rr] * (1.0f / 255.0f);
+                  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r1, vo1,
+                                                        ((32 * kt + (rr & 3) + 8 * (rr >> 2)) * 32) * 4, 0);
+              }
+              acc1[kt] = f32x16{};
+          }
         }
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt) sum1[kt] += acc1[kt];
         // conv1 bias partial of this wave: channel lane & 31, the two pixel halves of the B
         // fragments combined
         if constexpr (FI_C1B_PH2) {
@@ -1653,15 +1655,6 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                 for (int j = 0; j < 8; ++j) cs1[((size_t)blockIdx.x * 4 + wr) * 32 + 8 * g + j] = bs8[j];
             }
         }
-    }
-    if (w >= 4) {  // conv1 weight-gradient slab rows k = 32(2wr + kt) + (r&3) + 8(r>>2) + 4(lane>>5)
-        const float inv255 = 1.0f / 255.0f;
-        float* out1 = slab1 + (size_t)blockIdx.x * 256 * 32;
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-                out1[(32 * (2 * wr + kt) + (r & 3) + 8 * (r >> 2) + 4 * h) * 32 + col] = sum1[kt][r] * inv255;
     }
 }
 
