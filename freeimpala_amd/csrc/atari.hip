@@ -765,10 +765,10 @@ static bool dmalloc(AtariImpl* I, T** p, size_t n) {
 
 // split factors (blocks over the reduction) per weight-gradient GEMM
 constexpr int SPL_H = 128, SPL_FC = 9, SPL_C3 = 160, SPL_C2 = 256, SPL_C1 = 512;
-// partial weight-gradient slabs per frame-resident workgroup of the fused conv2 backward +
-// conv1 weight gradient (atari_fr.hip SEGS / C2_SEGS: blocked fp32 accumulation over the
-// workgroup's frames): conv2 [grid][kC2Segs][512][64], then conv1 [grid][kC1Segs][256][32]
-constexpr int kC2Segs = 2, kC1Segs = 8;
+// partial conv1 weight-gradient slabs per frame-resident workgroup of the fused conv2 backward +
+// conv1 weight gradient (atari_fr.hip SEGS: blocked fp32 accumulation over the workgroup's
+// frames): conv2 [grid][512][64], then conv1 [grid][kC1Segs][256][32]
+constexpr int kC1Segs = 8;
 constexpr int GBM = 128;  // M-tile of the dgrad GEMMs (class stride granularity)
 
 AtariNet* atari_create(int B, int T, int A) {
@@ -801,7 +801,7 @@ AtariNet* atari_create(int B, int T, int A) {
               dmalloc(I, &I->wb.c3D, 64 * 576) && dmalloc(I, &I->wb.fcB, (size_t)3136 * 512) &&
               dmalloc(I, &I->wb.hD, 512 * 32);
     const size_t s_fc = (size_t)SPL_FC * 3136 * 512, s_c3 = (size_t)SPL_C3 * 576 * 64,
-                 s_c2 = (size_t)SPL_C2 * (kC2Segs * 512 * 64 + kC1Segs * 256 * 32), s_c1 = (size_t)SPL_C1 * 256 * 32,
+                 s_c2 = (size_t)SPL_C2 * (512 * 64 + kC1Segs * 256 * 32), s_c1 = (size_t)SPL_C1 * 256 * 32,
                  s_h = (size_t)SPL_H * 512 * 32;
     I->slab_floats = std::max(std::max(s_fc, s_c3), std::max(std::max(s_c2, s_c1), s_h)) + 1024 * 512;
     ok = ok && dmalloc(I, &I->slab, I->slab_floats);
@@ -959,11 +959,11 @@ int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, con
     // conv2 backward + conv1 wgrad fused: da1 stays in LDS (written to HBM only with FI_KEEP_DA1)
     if (I->fr && I->fuse21) {
         const int grid = std::min(N, I->fr_grid);
-        float* slab1 = slab + (size_t)grid * kC2Segs * C2K * C2O;
+        float* slab1 = slab + (size_t)grid * C2K * C2O;
         float* cs1 = cs + (size_t)grid * C2O;
         FI_A("conv21_bwd", conv21_bwd_fr_launch(I->a1, I->da2, I->wb.c2D, frames, I->keep_da1 ? I->da1 : nullptr,
                                                 slab, cs + (size_t)3 * grid * C2O, slab1, cs1, Nb, grid, s, I->a1_planar));
-        FI_A("reduce_slabs", reduce_slabs(slab, grid * kC2Segs, (size_t)C2K * C2O, grads + o.c2w, s));
+        FI_A("reduce_slabs", reduce_slabs(slab, grid, (size_t)C2K * C2O, grads + o.c2w, s));
         FI_A("reduce_slabs", reduce_slabs(cs + (size_t)3 * grid * C2O, 2 * grid, (size_t)C2O, grads + o.c2b, s));
         FI_A("reduce_slabs", reduce_slabs(slab1, grid * kC1Segs, (size_t)C1K * C1O, grads + o.c1w, s));
         FI_A("reduce_slabs", reduce_slabs(cs1, 4 * grid, (size_t)C1O, grads + o.c1b, s));
@@ -975,7 +975,7 @@ int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, con
         const int grid = std::min(N, I->fr_grid);
         FI_A("conv2_bwd", conv2_bwd_fr_launch(I->a1, I->da2, I->wb.c2D, I->da1, slab, cs + (size_t)3 * grid * C2O, Nb,
                                               grid, s));
-        FI_A("reduce_slabs", reduce_slabs(slab, grid * kC2Segs, (size_t)C2K * C2O, grads + o.c2w, s));
+        FI_A("reduce_slabs", reduce_slabs(slab, grid, (size_t)C2K * C2O, grads + o.c2w, s));
         // the bias partials in the fused path's layout and place (bit-identical gradients)
         FI_A("reduce_slabs", reduce_slabs(cs + (size_t)3 * grid * C2O, 2 * grid, (size_t)C2O, grads + o.c2b, s));
     } else {

@@ -80,21 +80,19 @@ __device__ __forceinline__ f32x16 mfma_wg(const bf16x8& a, const bf16x8& b, f32x
 #endif
 }
 
-// Blocked fp32 accumulation of the persistent weight gradients. A workgroup walks ~1,616 frames
-// at the bench size; one fp32 accumulator chain over all of them (conv1's weight gradient: 25
-// MFMA steps per frame, ~40k accumulate roundings per element) measured 1.8e-5 relative L2
-// against fp64 (tests/test_gpu_atari.py, full size) -- over SURVEY.md's 1e-5 bar. So conv21_bwd_fr
-// walks its frames in SEGS contiguous segments (segment k ends after frame seg_last(k)) and
-// writes partial slabs at segment ends, outside the frame loop: conv1's weight gradient one per
-// segment, conv2's one per C2_EVERY segments (its error is ~4x smaller per frame); reduce_slabs
-// sums them in a fixed order. (A second conv1 register set, or the flush as a branch inside the
-// frame loop, each cost conv21 0.14-0.17 ms: profiles/r05_blocked_accumulation_ab.txt.)
+// Blocked fp32 accumulation of conv1's persistent weight gradient. A workgroup walks ~1,616
+// frames at the bench size; one fp32 accumulator chain over all of them (25 MFMA steps per
+// frame, ~40k accumulate roundings per element) measured 1.8e-5 relative L2 against fp64
+// (tests/test_gpu_atari.py, full size) -- over SURVEY.md's 1e-5 bar. conv21_bwd_fr's conv1 waves
+// therefore write a partial slab at the end of each of SEGS contiguous segments of their frames
+// (segment k ends after frame seg_last(k); empty segments write zero slabs) and reduce_slabs sums
+// them in a fixed order. conv2's weight gradient (6 MFMA steps per frame) stays one chain: it
+// measures 1.3e-6 with two segments and is within the bar whole. Measured alternatives
+// (profiles/r05_blocked_accumulation_ab.txt): a second conv1 register set, conv2 slabs flushed
+// from inside the frame loop, and both roles walking a segment loop nest cost conv21 0.14, 0.17
+// and 0.5 ms.
 constexpr int SEGS = 8;
-constexpr int C2_EVERY = 4;
-constexpr int C2_SEGS = SEGS / C2_EVERY;  // conv2 weight-gradient slabs per workgroup
 __device__ __forceinline__ int seg_last(int k, int nmine) { return ((k + 1) * nmine) / SEGS - 1; }
-// last frame of conv2 segment j (the end of segment C2_EVERY (j + 1) - 1)
-__device__ __forceinline__ int c2_seg_last(int j, int nmine) { return seg_last(C2_EVERY * (j + 1) - 1, nmine); }
 
 // one conv2 weight-gradient slab [512][64] from a wave's accumulators (kernel row wr), zeroing
 // them; with `drain` the stores (and every other outstanding VMEM op of the wave) complete
@@ -1060,7 +1058,7 @@ __global__ __launch_bounds__(512, 2) void conv2_bwd_fr(const __bf16* __restrict_
                                                        const __bf16* __restrict__ da2,
                                                        const __bf16* __restrict__ w2d,  // [4][32][256]
                                                        __bf16* __restrict__ da1,
-                                                       float* __restrict__ slab,     // [grid][C2_SEGS][512][64]
+                                                       float* __restrict__ slab,     // [grid][512][64]
                                                        float* __restrict__ cs_slab,  // [grid][64]
                                                        int nframes) {
     __shared__ __attribute__((aligned(16))) char smem[c2::RING * c2::SLOT + c2::SLOT / 16 * 4];
@@ -1083,12 +1081,6 @@ __global__ __launch_bounds__(512, 2) void conv2_bwd_fr(const __bf16* __restrict_
 #pragma unroll
         for (int t = 0; t < 4; ++t) { accw[t][0] = f32x16{}; accw[t][1] = f32x16{}; }
         float bsum0 = 0.f, bsum1 = 0.f;
-        const int nmine = nframes > (int)blockIdx.x ? (nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
-        float* const out = slab + (size_t)blockIdx.x * C2_SEGS * 512 * 64;
-        int it = 0, seg = 0;
-        // conv21_bwd_fr's conv2 slabs exactly: slab j holds frames (c2_seg_last(j - 1), c2_seg_last(j)],
-        // empty segments are zero slabs (bit-identical gradients, test_fused_conv21_...)
-        while (seg < C2_SEGS - 1 && c2_seg_last(seg, nmine) < 0) c2w_flush(accw, out + (size_t)seg++ * 512 * 64, wr, h, col, false);
         c2_frames(ctx, smem, 0, [&](const char* X, int) {
             // software pipeline: the 6 fragments of step ms+1 (12 transposed reads) are issued
             // between the 8 MFMAs of step ms; sched_group_barrier pins that interleave
@@ -1127,11 +1119,8 @@ __global__ __launch_bounds__(512, 2) void conv2_bwd_fr(const __bf16* __restrict_
                     }
                 }
             }
-            while (seg < C2_SEGS - 1 && it == c2_seg_last(seg, nmine))
-                c2w_flush(accw, out + (size_t)seg++ * 512 * 64, wr, h, col, true);
-            ++it;
         });
-        for (; seg < C2_SEGS; ++seg) c2w_flush(accw, out + (size_t)seg * 512 * 64, wr, h, col, false);
+        c2w_flush(accw, slab + (size_t)blockIdx.x * 512 * 64, wr, h, col, false);
         // lanes l and l+32 hold the same co (16*(g&1) + (l&15)), other m half; cs_slab has the
         // [grid][2][64] layout of conv21_bwd_fr's (row 1 zero), unless conv3_bwd fills it (FI_C2B_C3)
         if (!FI_C2B_C3 && wr == 0) {
@@ -1272,7 +1261,7 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                                                         const __bf16* __restrict__ w2d,  // [4][32][256]
                                                         const uint8_t* __restrict__ frames,
                                                         __bf16* __restrict__ da1_out,  // optional (parity checks)
-                                                        float* __restrict__ slab2,     // [grid][C2_SEGS][512][64]
+                                                        float* __restrict__ slab2,     // [grid][512][64]
                                                         float* __restrict__ cs2,       // [grid][2][64] (unless FI_C2B_C3)
                                                         float* __restrict__ slab1,     // [grid][SEGS][256][32]
                                                         float* __restrict__ cs1,       // [grid][4 waves][32]
@@ -1407,7 +1396,6 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
 #pragma unroll
         for (int t = 0; t < 4; ++t) { accw[t][0] = f32x16{}; accw[t][1] = f32x16{}; }
         float bsum0 = 0.f, bsum1_ = 0.f;
-        float* const out2 = slab2 + (size_t)blockIdx.x * C2_SEGS * 512 * 64;
         int issued = 0, m_dy = 0;
         if (nmine > 0) issued += issue_ax(0, 0);
         if (nmine > 1) issued += issue_ax(1, 1);
@@ -1417,9 +1405,7 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
             load_raw(0);
             issued += c21::NRAW_A;
         }
-        int it = 0;
-        for (int sg = 0; sg < SEGS; ++sg) {
-          for (const int stop = seg_last(sg, nmine) + 1; it < stop; ++it) {
+        for (int it = 0; it < nmine; ++it) {
             wait_vmcnt(issued - m_dy);  // own pieces of da2(it) landed (a1(it) is older)
             lds_barrier();  // B1: frame it's images in LDS; frame it-1's D and image consumed
             {
@@ -1484,10 +1470,9 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                 m_dy = issued;
             }
             if (it + 2 < nmine) issued += issue_ax(it + 2, it & 1);
-          }
-          // conv2 segment done: its partial slab out (the drain keeps the counted waits exact)
-          if ((sg + 1) % C2_EVERY == 0) c2w_flush(accw, out2 + (size_t)((sg + 1) / C2_EVERY - 1) * 512 * 64, wr, h, col, true);
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        c2w_flush(accw, slab2 + (size_t)blockIdx.x * 512 * 64, wr, h, col, false);
         if constexpr (!FI_C2B_C3) {  // cs2[block][0][64] (row [1] zero: the layout conv3_bwd fills otherwise)
             if (wr == 0) {
                 const float o0 = __shfl_xor(bsum0, 32, 64), o1 = __shfl_xor(bsum1_, 32, 64);
@@ -1528,9 +1513,27 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
         const int bd0 = 16 * (si + 128 * g + c2::zc(g));
         const int bd6 = 16 * (min(96 + si, 99) + 128 * g + c2::zc(g));
         float bs8[8] = {};  // !FI_C1B_PH2: conv1 bias partials, channels 8g + j of this lane's da1 pixels
-        int it = 0;
-        for (int sg = 0; sg < SEGS; ++sg) {
-          for (const int stop = seg_last(sg, nmine) + 1; it < stop; ++it) {
+        // conv1 segment slab out, rows k = 32(2wr + kt) + (r&3) + 8(r>>2) + 4(lane>>5) (x 1/255);
+        // plain buffer stores, no drain: these waves issue no counted DMA
+        int sg = 0;
+        auto c1_flush = [&]() {
+            const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc(
+                slab1 + ((size_t)blockIdx.x * SEGS + sg) * 256 * 32 + 64 * wr * 32, 0, 64 * 32 * 4, 0x00020000);
+            const int vo1 = fi_opaque((4 * h * 32 + col) * 4);
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+                for (int rr = 0; rr < 16; ++rr) {
+                    const float v = acc1[kt][rr] * (1.0f / 255.0f);
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r1, vo1,
+                                                          ((32 * kt + (rr & 3) + 8 * (rr >> 2)) * 32) * 4, 0);
+                }
+                acc1[kt] = f32x16{};
+            }
+            ++sg;
+        };
+        while (sg < SEGS && seg_last(sg, nmine) < 0) c1_flush();  // empty leading segments: zero slabs
+        for (int it = 0; it < nmine; ++it) {
             const int f = frame_of(it);
             lds_barrier();  // B1
             {  // conv2 data gradient of class (ty, tx) -> D (and da1_out)
@@ -1623,22 +1626,7 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                 case 2: conv1_wgrad(std::integral_constant<int, 2>{}); break;
                 default: conv1_wgrad(std::integral_constant<int, 3>{}); break;
             }
-          }
-          // conv1 segment done: its partial slab out, rows k = 32(2wr + kt) + (r&3) + 8(r>>2) +
-          // 4(lane>>5) (x 1/255). Plain stores: these waves issue no counted DMA
-          const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc(
-              slab1 + ((size_t)blockIdx.x * SEGS + sg) * 256 * 32 + 64 * wr * 32, 0, 64 * 32 * 4, 0x00020000);
-          const int vo1 = fi_opaque((4 * h * 32 + col) * 4);
-#pragma unroll
-          for (int kt = 0; kt < 2; ++kt) {
-#pragma unroll
-              for (int rr = 0; rr < 16; ++rr) {
-                  const float v = acc1[kt][rr] * (1.0f / 255.0f);
-                  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r1, vo1,
-                                                        ((32 * kt + (rr & 3) + 8 * (rr >> 2)) * 32) * 4, 0);
-              }
-              acc1[kt] = f32x16{};
-          }
+            while (sg < SEGS && it == seg_last(sg, nmine)) c1_flush();  // segment end (then empty ones)
         }
         // conv1 bias partial of this wave: channel lane & 31, the two pixel halves of the B
         // fragments combined
