@@ -92,6 +92,9 @@ __device__ __forceinline__ f32x16 mfma_wg(const bf16x8& a, const bf16x8& b, f32x
 // from inside the frame loop, and both roles walking a segment loop nest cost conv21 0.14, 0.17
 // and 0.5 ms.
 constexpr int SEGS = 8;
+#ifndef FI_EXP_C1F
+#define FI_EXP_C1F 0
+#endif
 __device__ __forceinline__ int seg_last(int k, int nmine) { return ((k + 1) * nmine) / SEGS - 1; }
 
 // one conv2 weight-gradient slab [512][64] from a wave's accumulators (kernel row wr), zeroing
@@ -1525,8 +1528,12 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
 #pragma unroll
                 for (int rr = 0; rr < 16; ++rr) {
                     const float v = acc1[kt][rr] * (1.0f / 255.0f);
+#if FI_EXP_C1F != 1  // 1: timing only, the segment slabs not stored (wrong conv1 gradient)
                     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r1, vo1,
                                                           ((32 * kt + (rr & 3) + 8 * (rr >> 2)) * 32) * 4, 0);
+#else
+                    asm volatile("" ::"v"(v));
+#endif
                 }
                 acc1[kt] = f32x16{};
             }
@@ -1626,7 +1633,11 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                 case 2: conv1_wgrad(std::integral_constant<int, 2>{}); break;
                 default: conv1_wgrad(std::integral_constant<int, 3>{}); break;
             }
+#if FI_EXP_C1F == 2  // timing only: the flush code present, never run (wrong conv1 gradient)
+            while (nframes < 0 && sg < SEGS && it == seg_last(sg, nmine)) c1_flush();
+#else
             while (sg < SEGS && it == seg_last(sg, nmine)) c1_flush();  // segment end (then empty ones)
+#endif
         }
         // conv1 bias partial of this wave: channel lane & 31, the two pixel halves of the B
         // fragments combined
