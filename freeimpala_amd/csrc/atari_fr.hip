@@ -59,6 +59,11 @@ constexpr int OUT = 400 * 32 * 2;                   // 25,600 B output / dY tile
 #ifndef FI_C21_PKMASK
 #define FI_C21_PKMASK 1
 #endif
+//   FI_C1_ONECOPY  conv21's conv1 weight gradient inlined once (every wave sums the bias of all
+//               m-steps, wave 4 stores it) instead of one copy per wave with the bias split
+#ifndef FI_C1_ONECOPY
+#define FI_C1_ONECOPY 0
+#endif
 // The weight gradients' 32x32x16 MFMA. FI_EXP_MFMA16 (timing only, WRONG results): the same
 // flops as two 16x16x32 MFMAs on the same operand registers into two quarters of the
 // accumulator, to price the MFMA shape's clock under the power limit (MI355X_MICROARCH.md:
@@ -1347,7 +1352,7 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
             for (int kt = 0; kt < 2; ++kt)
                 acc1[kt] = mfma_wg(cur[1 + kt], cur[0], acc1[kt]);
             if constexpr (FI_C1B_PH2) {
-                if ((ms & 3) == decltype(wrc)::value) bsum1 = sum8_bf16(cur[0], bsum1);
+                if (FI_C1_ONECOPY || (ms & 3) == decltype(wrc)::value) bsum1 = sum8_bf16(cur[0], bsum1);
             }
         }
     };
@@ -1626,12 +1631,16 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
             }
             lds_barrier();  // B2: D and the image complete
             if (it + 1 < nmine) load_raw(it + 1);
+#if FI_C1_ONECOPY  // one inlined copy: every wave sums all m-steps' bias (wave 4 writes it)
+            conv1_wgrad(std::integral_constant<int, 0>{});
+#else
             switch (wr) {  // the bias split is compile-time per wave (no branch in the m-step loop)
                 case 0: conv1_wgrad(std::integral_constant<int, 0>{}); break;
                 case 1: conv1_wgrad(std::integral_constant<int, 1>{}); break;
                 case 2: conv1_wgrad(std::integral_constant<int, 2>{}); break;
                 default: conv1_wgrad(std::integral_constant<int, 3>{}); break;
             }
+#endif
             // a segment ends here (at most one per frame once nmine >= SEGS; with fewer frames the
             // leading segments are empty and everything lands in the slabs flushed after the
             // loop). Marked unlikely: the block is placed out of the frame loop's code -- the
@@ -1643,7 +1652,7 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
         // fragments combined
         if constexpr (FI_C1B_PH2) {
             const float other = __shfl_xor(bsum1, 32, 64);
-            if (lane < 32) cs1[((size_t)blockIdx.x * 4 + wr) * 32 + lane] = bsum1 + other;
+            if (lane < 32) cs1[((size_t)blockIdx.x * 4 + wr) * 32 + lane] = FI_C1_ONECOPY && wr ? 0.f : bsum1 + other;
         } else {  // sum over the 16 lanes of each channel group
 #pragma unroll
             for (int j = 0; j < 8; ++j)
