@@ -31,7 +31,6 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef float f32x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
 
@@ -59,31 +58,6 @@ constexpr int OUT = 400 * 32 * 2;                   // 25,600 B output / dY tile
 #ifndef FI_C21_PKMASK
 #define FI_C21_PKMASK 1
 #endif
-//   FI_C1_ONECOPY  conv21's conv1 weight gradient inlined once (every wave sums the bias of all
-//               m-steps, wave 4 stores it) instead of one copy per wave with the bias split
-#ifndef FI_C1_ONECOPY
-#define FI_C1_ONECOPY 0
-#endif
-// The weight gradients' 32x32x16 MFMA. FI_EXP_MFMA16 (timing only, WRONG results): the same
-// flops as two 16x16x32 MFMAs on the same operand registers into two quarters of the
-// accumulator, to price the MFMA shape's clock under the power limit (MI355X_MICROARCH.md:
-// 16x16x32 loops hold a higher clock than 32x32x16 at equal cycles per FLOP).
-#ifndef FI_EXP_MFMA16
-#define FI_EXP_MFMA16 0
-#endif
-__device__ __forceinline__ f32x16 mfma_wg(const bf16x8& a, const bf16x8& b, f32x16 acc) {
-#if FI_EXP_MFMA16
-    f32x4 q0 = __builtin_shufflevector(acc, acc, 0, 1, 2, 3), q1 = __builtin_shufflevector(acc, acc, 4, 5, 6, 7);
-    q0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, q0, 0, 0, 0);
-    q1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, a, q1, 0, 0, 0);
-    const f32x4 r2 = __builtin_shufflevector(acc, acc, 8, 9, 10, 11), r3 = __builtin_shufflevector(acc, acc, 12, 13, 14, 15);
-    const f32x8 lo = __builtin_shufflevector(q0, q1, 0, 1, 2, 3, 4, 5, 6, 7);
-    const f32x8 hi = __builtin_shufflevector(r2, r3, 0, 1, 2, 3, 4, 5, 6, 7);
-    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
-#else
-    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
-#endif
-}
 
 // Blocked fp32 accumulation of conv1's persistent weight gradient. A workgroup walks ~1,616
 // frames at the bench size; one fp32 accumulator chain over all of them (25 MFMA steps per
@@ -97,9 +71,6 @@ __device__ __forceinline__ f32x16 mfma_wg(const bf16x8& a, const bf16x8& b, f32x
 // from inside the frame loop, and both roles walking a segment loop nest cost conv21 0.14, 0.17
 // and 0.5 ms.
 constexpr int SEGS = 8;
-#ifndef FI_EXP_C1F
-#define FI_EXP_C1F 0
-#endif
 __device__ __forceinline__ int seg_last(int k, int nmine) { return ((k + 1) * nmine) / SEGS - 1; }
 
 // one conv2 weight-gradient slab [512][64] from a wave's accumulators (kernel row wr), zeroing
@@ -400,7 +371,7 @@ __global__ __launch_bounds__(512, 2) void conv1_wgrad_fr(const uint8_t* __restri
             }
 #pragma unroll
             for (int kt = 0; kt < 4; ++kt)
-                acc[kt] = mfma_wg(cur[1 + kt], cur[0], acc[kt]);
+                acc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[1 + kt], cur[0], acc[kt], 0, 0, 0);
         };
         bf16x8 fb[2][5];
         load(0, fb[0]);
@@ -1115,8 +1086,8 @@ __global__ __launch_bounds__(512, 2) void conv2_bwd_fr(const __bf16* __restrict_
                 bsum1 = sum8_bf16(cur[1], bsum1);
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
-                    accw[t][0] = mfma_wg(cur[2 + t], cur[0], accw[t][0]);
-                    accw[t][1] = mfma_wg(cur[2 + t], cur[1], accw[t][1]);
+                    accw[t][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[2 + t], cur[0], accw[t][0], 0, 0, 0);
+                    accw[t][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[2 + t], cur[1], accw[t][1], 0, 0, 0);
                 }
 #pragma unroll
                 for (int k = 0; k < 8; ++k) {
@@ -1350,9 +1321,9 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
             const bf16x8* cur = fb[ms % (PD + 1)];
 #pragma unroll
             for (int kt = 0; kt < 2; ++kt)
-                acc1[kt] = mfma_wg(cur[1 + kt], cur[0], acc1[kt]);
+                acc1[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[1 + kt], cur[0], acc1[kt], 0, 0, 0);
             if constexpr (FI_C1B_PH2) {
-                if (FI_C1_ONECOPY || (ms & 3) == decltype(wrc)::value) bsum1 = sum8_bf16(cur[0], bsum1);
+                if ((ms & 3) == decltype(wrc)::value) bsum1 = sum8_bf16(cur[0], bsum1);
             }
         }
     };
@@ -1442,8 +1413,8 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                     }
 #pragma unroll
                     for (int t = 0; t < 4; ++t) {
-                        accw[t][0] = mfma_wg(cur[2 + t], cur[0], accw[t][0]);
-                        accw[t][1] = mfma_wg(cur[2 + t], cur[1], accw[t][1]);
+                        accw[t][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[2 + t], cur[0], accw[t][0], 0, 0, 0);
+                        accw[t][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[2 + t], cur[1], accw[t][1], 0, 0, 0);
                     }
 #pragma unroll
                     for (int k = 0; k < 8; ++k) {
@@ -1533,12 +1504,8 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
 #pragma unroll
                 for (int rr = 0; rr < 16; ++rr) {
                     const float v = acc1[kt][rr] * (1.0f / 255.0f);
-#if FI_EXP_C1F != 1  // 1: timing only, the segment slabs not stored (wrong conv1 gradient)
                     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r1, vo1,
                                                           ((32 * kt + (rr & 3) + 8 * (rr >> 2)) * 32) * 4, 0);
-#else
-                    asm volatile("" ::"v"(v));
-#endif
                 }
                 acc1[kt] = f32x16{};
             }
@@ -1631,16 +1598,12 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
             }
             lds_barrier();  // B2: D and the image complete
             if (it + 1 < nmine) load_raw(it + 1);
-#if FI_C1_ONECOPY  // one inlined copy: every wave sums all m-steps' bias (wave 4 writes it)
-            conv1_wgrad(std::integral_constant<int, 0>{});
-#else
             switch (wr) {  // the bias split is compile-time per wave (no branch in the m-step loop)
                 case 0: conv1_wgrad(std::integral_constant<int, 0>{}); break;
                 case 1: conv1_wgrad(std::integral_constant<int, 1>{}); break;
                 case 2: conv1_wgrad(std::integral_constant<int, 2>{}); break;
                 default: conv1_wgrad(std::integral_constant<int, 3>{}); break;
             }
-#endif
             // a segment ends here (at most one per frame once nmine >= SEGS; with fewer frames the
             // leading segments are empty and everything lands in the slabs flushed after the
             // loop). Marked unlikely: the block is placed out of the frame loop's code -- the
@@ -1652,7 +1615,7 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
         // fragments combined
         if constexpr (FI_C1B_PH2) {
             const float other = __shfl_xor(bsum1, 32, 64);
-            if (lane < 32) cs1[((size_t)blockIdx.x * 4 + wr) * 32 + lane] = FI_C1_ONECOPY && wr ? 0.f : bsum1 + other;
+            if (lane < 32) cs1[((size_t)blockIdx.x * 4 + wr) * 32 + lane] = bsum1 + other;
         } else {  // sum over the 16 lanes of each channel group
 #pragma unroll
             for (int j = 0; j < 8; ++j)
@@ -1881,8 +1844,8 @@ __device__ __forceinline__ void c3_wgrad(const C3Ctx& ctx, char* smem, float* sl
             bsum1 = sum8_bf16(cur[1], bsum1);
 #pragma unroll
             for (int i = 0; i < NKT; ++i) {
-                accw[i][0] = mfma_wg(cur[2 + i], cur[0], accw[i][0]);
-                accw[i][1] = mfma_wg(cur[2 + i], cur[1], accw[i][1]);
+                accw[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[2 + i], cur[0], accw[i][0], 0, 0, 0);
+                accw[i][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[2 + i], cur[1], accw[i][1], 0, 0, 0);
             }
             // 2NKT MFMAs, 2NKT + 4 reads of the next step: pairs of reads between MFMAs
 #pragma unroll
