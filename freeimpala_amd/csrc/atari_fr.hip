@@ -486,6 +486,12 @@ __device__ __forceinline__ int f3_dst(int i) {
 // bordered dY image 203 -> 104).
 __device__ __forceinline__ int rs_lane(int L) { return 8 * (L & 7) + ((2 * (L & 7) + (L >> 3)) & 7); }
 
+// a3's ReLU bitmask (conv_fwd_fr<3> writes it, conv3_bwd_fr reads it): one byte per 16-B
+// unit of a3 (pixel, 8-channel chunk), bit q = channel 8 chunk + q
+namespace c3m {
+constexpr int BYTES = 3136 / 8;  // 392 per frame
+}
+
 template <int L>  // L = 2 (conv2) or 3 (conv3)
 struct FwdGeo;
 template <>
@@ -508,6 +514,7 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
                                                       const __bf16* __restrict__ wt,   // [64][K] (ky,kx,ci)
                                                       const float* __restrict__ bias,  // [64]
                                                       __bf16* __restrict__ y,          // NHWC output frames
+                                                      uint8_t* __restrict__ ymask,     // L == 3: ReLU bitmask (see below)
                                                       int nframes) {
     using G = FwdGeo<L>;
     constexpr int K = G::KS * 32, FPI = G::FPI, STG = G::STG;
@@ -654,8 +661,20 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
                             ov[4 + r] = (__bf16)fmaxf(acc1[r] + bch[4 + r], 0.f);
                         }
                         u32x4* dst = (u32x4*)(y + (size_t)(blockIdx.x + k * gridDim.x) * G::OUT_ELEMS);
-                        FI_ST16(__builtin_bit_cast(u32x4, ov), dst + 8 * (G::OW * oy + ox) + 4 * chh + g);
+                        const int unit = 8 * (G::OW * oy + ox) + 4 * chh + g;
+                        FI_ST16(__builtin_bit_cast(u32x4, ov), dst + unit);
+                        if constexpr (L == 3) {
+                            // conv3_bwd_fr needs a3 only as the ReLU mask of da3: bit q of byte
+                            // `unit` = (a3 element 8 unit + q > 0), the predicate it applied to the
+                            // stored bf16 (392 B per frame instead of re-reading 6,272 B of a3)
+                            const s16x8 sv = __builtin_bit_cast(s16x8, ov);
+                            uint32_t m = 0;
+#pragma unroll
+                            for (int q = 0; q < 8; ++q) m |= sv[q] > 0 ? 1u << q : 0u;
+                            ymask[(size_t)(blockIdx.x + k * gridDim.x) * c3m::BYTES + unit] = (uint8_t)m;
+                        }
                     }
+                    if constexpr (L == 3) ++issued;  // the mask byte store
                 }
                 acc0 = f32x4{};
                 acc1 = f32x4{};
@@ -679,14 +698,15 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
 
 int conv2_fwd_fr_launch(const __bf16* a1, const __bf16* w2t, const float* bias, __bf16* a2, int nframes,
                         int grid, hipStream_t s) {
-    hipLaunchKernelGGL(conv_fwd_fr<2>, dim3(grid), dim3(512), 0, s, a1, w2t, bias, a2, nframes);
+    hipLaunchKernelGGL(conv_fwd_fr<2>, dim3(grid), dim3(512), 0, s, a1, w2t, bias, a2, (uint8_t*)nullptr, nframes);
     FI_HIP_CHECK(hipGetLastError());
     return FI_OK;
 }
 
-int conv3_fwd_fr_launch(const __bf16* a2, const __bf16* w3t, const float* bias, __bf16* a3, int nframes,
-                        int grid, hipStream_t s) {
-    hipLaunchKernelGGL(conv_fwd_fr<3>, dim3(grid), dim3(512), 0, s, a2, w3t, bias, a3, nframes);
+int conv3_fwd_fr_launch(const __bf16* a2, const __bf16* w3t, const float* bias, __bf16* a3, uint8_t* a3m,
+                        int nframes, int grid, hipStream_t s) {
+    FI_REQUIRE(a3m != nullptr, "conv3_fwd_fr: the a3 ReLU bitmask buffer is required");
+    hipLaunchKernelGGL(conv_fwd_fr<3>, dim3(grid), dim3(512), 0, s, a2, w3t, bias, a3, a3m, nframes);
     FI_HIP_CHECK(hipGetLastError());
     return FI_OK;
 }
@@ -1666,27 +1686,30 @@ __host__ __device__ constexpr int zc(int c) { return 8 * (c & 1) + 4 * ((c >> 1)
 }  // namespace c3
 
 struct C3Ctx {
-    const __bf16 *a2, *da3, *a3;
+    const __bf16 *a2, *da3;
+    const uint8_t* a3m;  // a3's ReLU bitmask (c3m)
     __bf16* da2;
     int nframes;
 };
 
-// Linear-DMA pipeline: every frame's a2, da3 and a3 arrive by LDS-DMA in their own byte order
-// (1 KiB contiguous per wave instruction) into one of two staging buffers; the issuing wave
-// then moves its own landed pieces into the frame's image slot (chunk-planar X, bordered dY),
-// applying the a3 ReLU mask to da3 on the way, so the mask image needs no slot. The gathered
+// Linear-DMA pipeline: every frame's a2, da3 and a3's ReLU bitmask arrive by LDS-DMA in their
+// own byte order (1 KiB contiguous per wave instruction) into one of two staging buffers; the
+// issuing wave then moves its own landed pieces into the frame's image slot (chunk-planar X,
+// bordered dY), applying the a3 mask to da3 on the way, so the mask image needs no slot. (Round
+// 5: the mask is conv_fwd_fr<3>'s 392-byte bitmask, one piece on wave 3, instead of a3 itself,
+// 7 pieces / 6,272 B per frame.) The gathered
 // DMA straight into the image layouts issued 16-byte pieces at a 128-byte
 // stride: the same bytes, 8x the memory requests (timing with linear sources and wrong
 // layouts: 4.29 -> 3.85 ms; the gathered form is no longer built).
 // LDS: 2 image slots (X + dY, 28,672 B each; gap / border units zeroed once, never written),
-// 2 staging buffers (a2 11 + da3 7 + a3 7 pieces of 1 KiB), destination tables: 110,624 B.
+// 2 staging buffers (a2 11 + da3 7 + bitmask 1 pieces of 1 KiB), destination tables: 98,336 B.
 namespace c3 {
 constexpr int SLOT2 = XB + DYB;                    // 28,672
-constexpr int NPX = 11, NPD = 7;                   // 1-KiB pieces of a2, of da3 (= of a3)
-constexpr int STGB = (NPX + 2 * NPD) * 1024;       // 25,600
+constexpr int NPX = 11, NPD = 7;                   // 1-KiB pieces of a2, of da3
+constexpr int STGB = (NPX + NPD + 1) * 1024;       // 19,456 (+ one piece: the a3 bitmask)
 constexpr int NUX = 10368 / 16, NUD = 6272 / 16;   // 16-B units of a2, of da3
 constexpr int O_STG = 2 * SLOT2, O_TAB = O_STG + 2 * STGB;
-constexpr int LDS = O_TAB + (NUX + NUD) * 2;       // 110,624
+constexpr int LDS = O_TAB + (NUX + NUD) * 2;       // 98,336
 }  // namespace c3
 
 // ISSUER: waves 0-3 (compile-time role, so the data-gradient waves carry none of the DMA /
@@ -1712,7 +1735,7 @@ __device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, int nst, W
         const int f = blockIdx.x + k * gridDim.x;
         const fi_i32x4 xr = make_rsrc(c.a2 + (size_t)f * 5184, 10368);
         const fi_i32x4 dr = make_rsrc(c.da3 + (size_t)f * 3136, 6272);
-        const fi_i32x4 mr = make_rsrc(c.a3 + (size_t)f * 3136, 6272);
+        const fi_i32x4 mr = make_rsrc(c.a3m + (size_t)f * c3m::BYTES, c3m::BYTES);
         const uint32_t base = lds0 + c3::O_STG + sb * c3::STGB;
         int n = 0;
 #pragma unroll
@@ -1728,9 +1751,12 @@ __device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, int nst, W
             const int j = w + 4 * i;
             if (j < c3::NPD) {
                 blds16(dr, 1024 * j + 16 * lane, base + 1024 * (c3::NPX + j));
-                blds16(mr, 1024 * j + 16 * lane, base + 1024 * (c3::NPX + c3::NPD + j));
-                n += 2;
+                ++n;
             }
+        }
+        if (w == 3) {  // the bitmask (392 B; lanes past it read zeros): wave 3 has the fewest pieces
+            blds16(mr, 16 * lane, base + 1024 * (c3::NPX + c3::NPD));
+            ++n;
         }
         return n;
     };
@@ -1751,13 +1777,14 @@ __device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, int nst, W
             for (int i = 0; i < 3; ++i)
                 if (64 * (w + 4 * i) + sl < c3::NUX) *(u32x4*)(im + 16 * xd[i]) = xv[i];
         }
-        s16x8 dv[2], mv[2];
+        s16x8 dv[2];
+        uint32_t mb[2];
         int dd[2];
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int u = min(64 * (w + 4 * i) + sl, c3::NUD - 1);
             dv[i] = *(const s16x8*)(st + 1024 * c3::NPX + 16 * u);
-            mv[i] = *(const s16x8*)(st + 1024 * (c3::NPX + c3::NPD) + 16 * u);
+            mb[i] = *(const uint8_t*)(st + 1024 * (c3::NPX + c3::NPD) + u);
             dd[i] = dsty[u];
         }
 #pragma unroll
@@ -1765,7 +1792,7 @@ __device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, int nst, W
             if (64 * (w + 4 * i) + sl < c3::NUD) {
                 s16x8 v = dv[i];
 #pragma unroll
-                for (int q = 0; q < 8; ++q) v[q] = mv[i][q] > 0 ? v[q] : (short)0;
+                for (int q = 0; q < 8; ++q) v[q] = (mb[i] >> q) & 1u ? v[q] : (short)0;
                 *(s16x8*)(im + c3::XB + 16 * dd[i]) = v;
             }
     };
@@ -1881,7 +1908,7 @@ __device__ __forceinline__ void c3_wgrad(const C3Ctx& ctx, char* smem, float* sl
 
 __global__ __launch_bounds__(512, 2) void conv3_bwd_fr(const __bf16* __restrict__ a2,
                                                        const __bf16* __restrict__ da3,  // unmasked
-                                                       const __bf16* __restrict__ a3,   // its mask
+                                                       const uint8_t* __restrict__ a3m,  // its mask (c3m)
                                                        const __bf16* __restrict__ w3d,  // [64 ci][576]
                                                        __bf16* __restrict__ da2,
                                                        float* __restrict__ slab,     // [grid][576][64]
@@ -1892,7 +1919,7 @@ __global__ __launch_bounds__(512, 2) void conv3_bwd_fr(const __bf16* __restrict_
     const int lane = threadIdx.x & 63;
     const int w = wave_id(), wr = w & 3;
     const int g = lane >> 4;
-    const C3Ctx ctx{a2, da3, a3, da2, nframes};
+    const C3Ctx ctx{a2, da3, a3m, da2, nframes};
 
     if (w < 4) {
         if (wr >> 1) c3_wgrad<1>(ctx, smem, slab, cs_slab, wr);
@@ -2001,9 +2028,10 @@ __global__ __launch_bounds__(512, 2) void conv3_bwd_fr(const __bf16* __restrict_
     }
 }
 
-int conv3_bwd_fr_launch(const __bf16* a2, const __bf16* da3, const __bf16* a3, const __bf16* w3d, __bf16* da2,
+int conv3_bwd_fr_launch(const __bf16* a2, const __bf16* da3, const uint8_t* a3m, const __bf16* w3d, __bf16* da2,
                         float* slab, float* cs_slab, float* cs2, int nframes, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(conv3_bwd_fr, dim3(grid), dim3(512), 0, s, a2, da3, a3, w3d, da2,
+    FI_REQUIRE(a3m != nullptr, "conv3_bwd_fr: the a3 ReLU bitmask is required");
+    hipLaunchKernelGGL(conv3_bwd_fr, dim3(grid), dim3(512), 0, s, a2, da3, a3m, w3d, da2,
                        slab, cs_slab, cs2, nframes);
     FI_HIP_CHECK(hipGetLastError());
     return FI_OK;
