@@ -1696,20 +1696,21 @@ struct C3Ctx {
 // own byte order (1 KiB contiguous per wave instruction) into one of two staging buffers; the
 // issuing wave then moves its own landed pieces into the frame's image slot (chunk-planar X,
 // bordered dY), applying the a3 mask to da3 on the way, so the mask image needs no slot. (Round
-// 5: the mask is conv_fwd_fr<3>'s 392-byte bitmask, one piece on wave 3, instead of a3 itself,
-// 7 pieces / 6,272 B per frame.) The gathered
+// 5: the mask is conv_fwd_fr<3>'s 392-byte bitmask, one piece per issuing wave, instead of a3
+// itself, 7 pieces / 6,272 B per frame.) The gathered
 // DMA straight into the image layouts issued 16-byte pieces at a 128-byte
 // stride: the same bytes, 8x the memory requests (timing with linear sources and wrong
 // layouts: 4.29 -> 3.85 ms; the gathered form is no longer built).
 // LDS: 2 image slots (X + dY, 28,672 B each; gap / border units zeroed once, never written),
-// 2 staging buffers (a2 11 + da3 7 + bitmask 1 pieces of 1 KiB), destination tables: 98,336 B.
+// 2 staging buffers (a2 11 + da3 7 + 4 bitmask copies, pieces of 1 KiB), destination tables:
+// 104,480 B.
 namespace c3 {
 constexpr int SLOT2 = XB + DYB;                    // 28,672
 constexpr int NPX = 11, NPD = 7;                   // 1-KiB pieces of a2, of da3
-constexpr int STGB = (NPX + NPD + 1) * 1024;       // 19,456 (+ one piece: the a3 bitmask)
+constexpr int STGB = (NPX + NPD + 4) * 1024;       // 22,528 (+ the a3 bitmask, one copy per issuing wave)
 constexpr int NUX = 10368 / 16, NUD = 6272 / 16;   // 16-B units of a2, of da3
 constexpr int O_STG = 2 * SLOT2, O_TAB = O_STG + 2 * STGB;
-constexpr int LDS = O_TAB + (NUX + NUD) * 2;       // 98,336
+constexpr int LDS = O_TAB + (NUX + NUD) * 2;       // 104,480
 }  // namespace c3
 
 // ISSUER: waves 0-3 (compile-time role, so the data-gradient waves carry none of the DMA /
@@ -1754,11 +1755,11 @@ __device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, int nst, W
                 ++n;
             }
         }
-        if (w == 3) {  // the bitmask (392 B; lanes past it read zeros): wave 3 has the fewest pieces
-            blds16(mr, 16 * lane, base + 1024 * (c3::NPX + c3::NPD));
-            ++n;
-        }
-        return n;
+        // the whole bitmask (392 B; lanes past it read zeros) into this wave's own copy: the
+        // reshuffle below runs right after the wave's OWN vmcnt wait, so it may only read pieces
+        // this wave issued (one shared copy from one wave raced the other waves' reads)
+        blds16(mr, 16 * lane, base + 1024 * (c3::NPX + c3::NPD + w));
+        return n + 1;
     };
     const int sl = rs_lane(lane);  // lane order with bank-conflict-free write groups
     auto reshuffle = [&](int sb, int slot) {  // own landed pieces -> image slot (a2, then da3: reads, then writes)
@@ -1784,7 +1785,7 @@ __device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, int nst, W
         for (int i = 0; i < 2; ++i) {
             const int u = min(64 * (w + 4 * i) + sl, c3::NUD - 1);
             dv[i] = *(const s16x8*)(st + 1024 * c3::NPX + 16 * u);
-            mb[i] = *(const uint8_t*)(st + 1024 * (c3::NPX + c3::NPD) + u);
+            mb[i] = *(const uint8_t*)(st + 1024 * (c3::NPX + c3::NPD + w) + u);
             dd[i] = dsty[u];
         }
 #pragma unroll
