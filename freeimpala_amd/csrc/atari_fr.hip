@@ -522,7 +522,13 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
     constexpr int NLP = (G::IN_BYTES + 1023) / 1024;   // 1-KiB pieces per input frame
     constexpr int PPW = (NLP + 7) / 8;                  // pieces per wave per frame (at most)
     constexpr int IMG = 2 * FPI * G::XB, SBUF = FPI * NLP * 1024;
-    __shared__ __attribute__((aligned(16))) char smem[IMG + STG * SBUF + NLP * 64 * 2];
+    // L == 3: the iterations' a3 ReLU bitmasks (2 x FPI x 392 B), staged in LDS so that each frame's
+    // 392 bytes leave as one 16-B-per-lane store (one byte store per lane from the epilogue --
+    // partial lines -- cost conv3_fwd 0.17 ms)
+    constexpr int MSTR = 400;  // per-frame stride in LDS (392 rounded up to 16 B: aligned b128 reads)
+    constexpr int MBUF = L == 3 ? 2 * FPI * MSTR : 0;
+    __shared__ __attribute__((aligned(16))) char smem[IMG + STG * SBUF + NLP * 64 * 2 + MBUF];
+    uint8_t* const mbuf = (uint8_t*)(smem + IMG + STG * SBUF + NLP * 64 * 2);
     const int lane = threadIdx.x & 63, tid = threadIdx.x;
     const int w = wave_id(), chh = w >> 2, pg = w & 3;
     const int g = lane >> 4, c16 = lane & 15, si = c16 ^ ((c16 >> 1) & 4);
@@ -626,9 +632,31 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
         }
     };
     constexpr int NSTEP = TPW * G::KS;  // (tile, k-step) steps per iteration
+    // wave 0 stores iteration i2's bitmasks (complete once every wave has passed the next barrier):
+    // lanes 0..24 of one 16-B store per frame, the descriptor's 392-B range drops the rest
+    auto store_masks = [&](int i2) {
+        int n = 0;
+        if constexpr (L == 3) {
+            if (w == 0) {
+#pragma unroll
+                for (int u = 0; u < FPI; ++u) {
+                    const int k = FPI * i2 + u;
+                    if (k < nmine) {
+                        const u32x4 v = *(const u32x4*)(mbuf + ((i2 & 1) * FPI + u) * MSTR + 16 * min(lane, 24));
+                        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+                            ymask + (size_t)(blockIdx.x + k * gridDim.x) * c3m::BYTES, 0, c3m::BYTES, 0x00020000);
+                        __builtin_amdgcn_raw_buffer_store_b128(v, r, 16 * lane, 0, 0);
+                        ++n;
+                    }
+                }
+            }
+        }
+        return n;
+    };
     for (int it = 0; it < niter; ++it) {
         const char* X = smem + (it & 1) * FPI * G::XB;
         lds_barrier();  // iteration it's image written; iteration it-1 consumed by every wave
+        if (it > 0) issued += store_masks(it - 1);
         // tile-outer steps: each tile's 2*KS MFMAs end in its 16-byte store; B fragments are
         // read PD steps ahead of their MFMAs
         constexpr int PD = 4;
@@ -671,10 +699,9 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
                             uint32_t m = 0;
 #pragma unroll
                             for (int q = 0; q < 8; ++q) m |= sv[q] > 0 ? 1u << q : 0u;
-                            ymask[(size_t)(blockIdx.x + k * gridDim.x) * c3m::BYTES + unit] = (uint8_t)m;
+                            mbuf[((it & 1) * FPI + fi) * MSTR + unit] = (uint8_t)m;
                         }
                     }
-                    if constexpr (L == 3) ++issued;  // the mask byte store
                 }
                 acc0 = f32x4{};
                 acc1 = f32x4{};
@@ -692,6 +719,12 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
 #pragma unroll
         for (int q = 0; q + 1 < STG; ++q) mk[q] = mk[q + 1];
         mk[STG - 1] = mnew;
+    }
+    if constexpr (L == 3) {
+        if (niter > 0) {
+            __syncthreads();  // the last iteration's bitmask bytes written by every wave
+            store_masks(niter - 1);
+        }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
