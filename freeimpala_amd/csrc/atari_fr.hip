@@ -96,17 +96,6 @@ __device__ __forceinline__ void c2w_flush(f32x16 (&accw)[4][2], float* out, int 
     if (drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// Loop-tail conditions (true on every frame but the last one or two): FI_LIKELY_HINTS=1 marks
-// them likely, so the block layout keeps the per-frame path fall-through (A/B)
-#ifndef FI_LIKELY_HINTS
-#define FI_LIKELY_HINTS 0
-#endif
-#if FI_LIKELY_HINTS
-#define FI_HOT(x) __builtin_expect(!!(x), 1)
-#else
-#define FI_HOT(x) (x)
-#endif
-
 // sum of a fragment's 8 bf16 values into acc: 4 v_dot2c_f32_bf16 against (1, 1) instead of 8
 // conversions + 8 adds (the weight-gradient waves' bias column sums of dY)
 __device__ __forceinline__ float sum8_bf16(const bf16x8& v, float acc) {
@@ -643,23 +632,21 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
         }
     };
     constexpr int NSTEP = TPW * G::KS;  // (tile, k-step) steps per iteration
-    // wave 0 stores iteration i2's bitmasks (complete once every wave has passed the next barrier):
-    // lanes 0..24 of one 16-B store per frame, the descriptor's 392-B range drops the rest
-    auto store_masks = [&](int i2) {
+    // wave u < FPI stores frame u of iteration i2's bitmasks (complete once every wave has passed
+    // the next barrier): lanes 0..24 of one 16-B store, the descriptor's 392-B range drops the
+    // rest. The LDS read happens right after that barrier, the store after the MFMA pipeline.
+    auto load_masks = [&](int i2) {
+        return *(const u32x4*)(mbuf + ((i2 & 1) * FPI + min(w, FPI - 1)) * MSTR + 16 * min(lane, 24));
+    };
+    auto store_masks = [&](int i2, const u32x4& v) {
         int n = 0;
         if constexpr (L == 3) {
-            if (w == 0) {
-#pragma unroll
-                for (int u = 0; u < FPI; ++u) {
-                    const int k = FPI * i2 + u;
-                    if (k < nmine) {
-                        const u32x4 v = *(const u32x4*)(mbuf + ((i2 & 1) * FPI + u) * MSTR + 16 * min(lane, 24));
-                        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-                            ymask + (size_t)(blockIdx.x + k * gridDim.x) * c3m::BYTES, 0, c3m::BYTES, 0x00020000);
-                        __builtin_amdgcn_raw_buffer_store_b128(v, r, 16 * lane, 0, 0);
-                        ++n;
-                    }
-                }
+            const int k = FPI * i2 + w;
+            if (w < FPI && k < nmine) {
+                const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+                    ymask + (size_t)(blockIdx.x + k * gridDim.x) * c3m::BYTES, 0, c3m::BYTES, 0x00020000);
+                __builtin_amdgcn_raw_buffer_store_b128(v, r, 16 * lane, 0, 0);
+                ++n;
             }
         }
         return n;
@@ -667,7 +654,10 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
     for (int it = 0; it < niter; ++it) {
         const char* X = smem + (it & 1) * FPI * G::XB;
         lds_barrier();  // iteration it's image written; iteration it-1 consumed by every wave
-        if (it > 0) issued += store_masks(it - 1);
+        u32x4 mprev = u32x4{0, 0, 0, 0};
+        if constexpr (L == 3) {
+            if (it > 0 && w < FPI) mprev = load_masks(it - 1);
+        }
         // tile-outer steps: each tile's 2*KS MFMAs end in its 16-byte store; B fragments are
         // read PD steps ahead of their MFMAs
         constexpr int PD = 4;
@@ -676,7 +666,8 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
         for (int st = 0; st < PD; ++st) fb[st] = *(const bf16x8*)(X + bbase[st / G::KS] + imm(st % G::KS));
         __builtin_amdgcn_sched_group_barrier(0x100, PD, 0);
         f32x4 acc0 = f32x4{}, acc1 = f32x4{};
-        uint32_t mreg[TPW];  // L == 3: tile i's mask byte | unit << 8 | frame << 24 | valid << 31
+        uint32_t mreg[TPW];  // L == 3: tile i's unit << 8 | frame << 24 | valid << 31
+        u32x4 vreg[TPW];     // ... and its 8 stored a3 values
 #pragma unroll
         for (int i = 0; i < TPW; ++i) mreg[i] = 0;
 #pragma unroll
@@ -706,22 +697,11 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
                         const int unit = 8 * (G::OW * oy + ox) + 4 * chh + g;
                         FI_ST16(__builtin_bit_cast(u32x4, ov), dst + unit);
                         if constexpr (L == 3) {
-                            // conv3_bwd_fr needs a3 only as the ReLU mask of da3: bit q of byte
-                            // `unit` = (a3 element 8 unit + q > 0), the predicate it applied to the
-                            // stored bf16 (392 B per frame instead of re-reading 6,272 B of a3).
-                            // 0 - x with i16 saturation is negative exactly for x > 0: the sign
-                            // bits of one v_pk_sub_i16 per pair are the pair's two mask bits. Kept
-                            // in a register: an LDS write here, inside the prefetched B-fragment
-                            // pipeline, cost conv3_fwd 0.16 ms
-                            const u32x4 dv = __builtin_bit_cast(u32x4, ov);
-                            uint32_t m = 0;
-#pragma unroll
-                            for (int j = 0; j < 4; ++j) {
-                                uint32_t t;
-                                asm("v_pk_sub_i16 %0, 0, %1 clamp" : "=v"(t) : "v"(dv[j]));
-                                m |= ((t >> 15) & 1u) << (2 * j) | ((t >> 31) & 1u) << (2 * j + 1);
-                            }
-                            mreg[i] = m | (uint32_t)unit << 8 | (uint32_t)fi << 24 | 1u << 31;
+                            // kept for the bitmask, which is built after the MFMA pipeline (an LDS
+                            // write here, inside the prefetched B-fragment pipeline, cost
+                            // conv3_fwd 0.16 ms)
+                            vreg[i] = __builtin_bit_cast(u32x4, ov);
+                            mreg[i] = (uint32_t)unit << 8 | (uint32_t)fi << 24 | 1u << 31;
                         }
                     }
                 }
@@ -729,18 +709,32 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
                 acc1 = f32x4{};
             }
         }
-        if constexpr (L == 3) {  // this iteration's mask bytes into LDS, after the MFMA pipeline
+        if constexpr (L == 3) {
+            // this iteration's mask bytes into LDS, after the MFMA pipeline. conv3_bwd_fr needs a3
+            // only as the ReLU mask of da3: bit q of byte `unit` = (a3 element 8 unit + q > 0), the
+            // predicate it applied to the stored bf16 (392 B per frame instead of re-reading
+            // 6,272 B of a3). 0 - x with i16 saturation is negative exactly for x > 0: the sign
+            // bits of one v_pk_sub_i16 per pair are the pair's two mask bits
 #pragma unroll
             for (int i = 0; i < TPW; ++i)
-                if (mreg[i] >> 31)
-                    mbuf[((it & 1) * FPI + ((mreg[i] >> 24) & 0x7f)) * MSTR + ((mreg[i] >> 8) & 0xffff)] = (uint8_t)mreg[i];
+                if (mreg[i] >> 31) {
+                    uint32_t m = 0;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        uint32_t t;
+                        asm("v_pk_sub_i16 %0, 0, %1 clamp" : "=v"(t) : "v"(vreg[i][j]));
+                        m |= ((t >> 15) & 1u) << (2 * j) | ((t >> 31) & 1u) << (2 * j + 1);
+                    }
+                    mbuf[((it & 1) * FPI + ((mreg[i] >> 24) & 0x7f)) * MSTR + ((mreg[i] >> 8) & 0xffff)] = (uint8_t)m;
+                }
+            if (it > 0) issued += store_masks(it - 1, mprev);
         }
-        if (FI_HOT(it + 1 < niter)) {
+        if (it + 1 < niter) {
             wait_vmcnt(issued - mk[0]);  // own pieces of iteration it + 1 landed (stores may fly)
             reshuffle(it + 1);           // image slot (it+1)&1 was last read in iteration it-1
         }
         int mnew = issued;
-        if (FI_HOT(it + 1 + STG < niter)) {
+        if (it + 1 + STG < niter) {
             issued += issue(it + 1 + STG);  // into the staging buffer just emptied
             mnew = issued;
         }
@@ -751,7 +745,7 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
     if constexpr (L == 3) {
         if (niter > 0) {
             __syncthreads();  // the last iteration's bitmask bytes written by every wave
-            store_masks(niter - 1);
+            if (w < FPI) store_masks(niter - 1, load_masks(niter - 1));
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -840,14 +834,14 @@ __global__ __launch_bounds__(512, 2) void conv12_fwd_fr(const uint8_t* __restric
         for (int it = 0; it <= nmine; ++it) {
             const int f = blockIdx.x + it * gridDim.x;
             lds_barrier();  // B1: raw(it) landed (waited by its issuers); conv1 image and a1 image free
-            if (FI_HOT(it >= 1)) {  // a1(it-1) -> conv2 image (pixel q, chunk g)
+            if (it >= 1) {  // a1(it-1) -> conv2 image (pixel q, chunk g)
 #pragma unroll
                 for (int tt = 0; tt < 7; ++tt)
                     if (tt < ntile) *(u32x4*)(x2 + 16 * f2_dst(4 * ((w + 4 * tt) * 16 + si) + g)) = held[tt];
             }
-            if (FI_HOT(it < nmine)) c12_convert(smem + (it & 1) * c1::RAW, img, tid);
+            if (it < nmine) c12_convert(smem + (it & 1) * c1::RAW, img, tid);
             lds_barrier();  // B2: conv1 image and conv2 image complete
-            if (FI_HOT(it < nmine)) {
+            if (it < nmine) {
                 u32x4* dst = (u32x4*)(a1 + (size_t)f * 12800);
                 auto load = [&](int t, bf16x8* d) {
                     const int q = t * 16 + si, oy = q / 20, ox = q - 20 * oy;
@@ -932,16 +926,16 @@ __global__ __launch_bounds__(512, 2) void conv12_fwd_fr(const uint8_t* __restric
         if (nmine > 1) issued += issue_raw(1, 1);
         m1 = issued;
         for (int it = 0; it <= nmine; ++it) {
-            if (FI_HOT(it < nmine)) wait_vmcnt(issued - m0);  // own pieces of raw(it) landed
+            if (it < nmine) wait_vmcnt(issued - m0);  // own pieces of raw(it) landed
             lds_barrier();  // B1
-            if (FI_HOT(it < nmine)) c12_convert(smem + (it & 1) * c1::RAW, img, tid);
+            if (it < nmine) c12_convert(smem + (it & 1) * c1::RAW, img, tid);
             lds_barrier();  // B2: raw slot it&1 converted; a1(it-1) in the conv2 image
             int m2 = issued;
-            if (FI_HOT(it + 2 < nmine)) {
+            if (it + 2 < nmine) {
                 issued += issue_raw(it + 2, it & 1);
                 m2 = issued;
             }
-            if (FI_HOT(it >= 1)) {  // conv2 of frame it-1 from the a1 image
+            if (it >= 1) {  // conv2 of frame it-1 from the a1 image
                 const int k = it - 1;
                 u32x4* dst = (u32x4*)(a2 + (size_t)(blockIdx.x + k * gridDim.x) * 5184);
                 constexpr int PD = 4, NSTEP = 3 * 16;
@@ -1520,16 +1514,16 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
             // raw(it + 1) goes out now, while this wave waits at B2 for the data-gradient
             // waves: in phase 2 its issue would queue behind the DMA (several thousand clocks
             // of issue stall per frame with both there)
-            if (FI_HOT(it + 1 < nmine)) {
+            if (it + 1 < nmine) {
                 load_raw(it + 1);
                 issued += c21::NRAW_A;
             }
             lds_barrier();  // B2: D and the image complete; da2 image and a1 slot it&1 consumed
-            if (FI_HOT(it + 1 < nmine)) {
+            if (it + 1 < nmine) {
                 issued += issue_dy(it + 1);
                 m_dy = issued;
             }
-            if (FI_HOT(it + 2 < nmine)) issued += issue_ax(it + 2, it & 1);
+            if (it + 2 < nmine) issued += issue_ax(it + 2, it & 1);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         c2w_flush(accw, slab2 + (size_t)blockIdx.x * 512 * 64, wr, h, col, false);
@@ -1678,7 +1672,7 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                 }
             }
             lds_barrier();  // B2: D and the image complete
-            if (FI_HOT(it + 1 < nmine)) load_raw(it + 1);
+            if (it + 1 < nmine) load_raw(it + 1);
             switch (wr) {  // the bias split is compile-time per wave (no branch in the m-step loop)
                 case 0: conv1_wgrad(std::integral_constant<int, 0>{}); break;
                 case 1: conv1_wgrad(std::integral_constant<int, 1>{}); break;
@@ -1878,11 +1872,11 @@ __device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, int nst, W
         const int f = blockIdx.x + it * gridDim.x;
         char* X = smem + (it & 1) * c3::SLOT2;
         lds_barrier();  // frame it in slot it&1; every wave done with frame it-1 (slot (it+1)&1)
-        if (ISSUER && FI_HOT(it + 1 < nmine)) {
+        if (ISSUER && it + 1 < nmine) {
             wait_vmcnt(issued - mA);  // own pieces of frame it+1 landed
             reshuffle((it + 1) & 1, (it + 1) & 1);
             int mC = issued;
-            if (FI_HOT(it + 3 < nmine)) {
+            if (it + 3 < nmine) {
                 issued += issue(it + 3, (it + 1) & 1);  // into the staging buffer just emptied
                 mC = issued;
             }
