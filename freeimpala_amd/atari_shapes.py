@@ -13,7 +13,6 @@ A1 = 20 * 20 * 32 * 2    # bf16 bytes per frame: a1 / da1
 A2 = 9 * 9 * 64 * 2      # a2 / da2
 A3 = 7 * 7 * 64 * 2      # a3 / da3
 H = 512 * 2              # h / dh
-A3M = 7 * 7 * 64 // 8    # a3's ReLU bitmask (frame-resident path): one bit per element
 
 
 def atari_kernel_work(T: int, B: int, A: int) -> dict:
@@ -28,7 +27,7 @@ def atari_kernel_work(T: int, B: int, A: int) -> dict:
     return {
         "conv1_fwd": (c1, N * (FRAME + A1)),
         "conv2_fwd": (c2, N * (A1 + A2)),
-        "conv3_fwd": (c3, N * (A2 + A3 + A3M)),   # frame-resident: also writes a3's bitmask
+        "conv3_fwd": (c3, N * (A2 + A3)),
         "fc_fwd": (fc, N * (A3 + H)),
         "heads_fwd": (hd, N * (H + 4 * O)),
         "heads_wgrad": (hd, N * (H + 4 * O)),
@@ -41,10 +40,9 @@ def atari_kernel_work(T: int, B: int, A: int) -> dict:
         "conv2_dgrad": (c2, N * (A2 + 2 * A1)),
         "conv1_wgrad": (c1, N * (FRAME + A1)),
         # fused frame-resident backward kernels (wgrad + dgrad + bias of the layer):
-        # conv3 reads a2, da3 (unmasked) and a3's ReLU bitmask, writes da2; conv2 reads a1, da2,
-        # writes da1
+        # conv3 reads a2, da3 (unmasked) and its mask a3, writes da2; conv2 reads a1, da2, writes da1
         "conv2_bwd": (2 * c2, N * (A1 + A2 + A1)),
-        "conv3_bwd": (2 * c3, N * (A2 + A3 + A3M + A2)),
+        "conv3_bwd": (2 * c3, N * (A2 + 2 * A3 + A2)),
         # fused conv1 + conv2 forward: frames in, a1 and a2 out (a1 is not read back)
         "conv12_fwd": (c1 + c2, N * (FRAME + A1 + A2)),
         # fused conv2 backward + conv1 weight gradient: a1, da2, frames in (da1 stays in LDS)

@@ -718,7 +718,6 @@ struct AtariImpl {
     WeightsBf16 wb{};
     __bf16 *a1 = nullptr, *a2 = nullptr, *a3 = nullptr, *h = nullptr;
     __bf16 *da1 = nullptr, *da2 = nullptr, *da3 = nullptr, *dh = nullptr;
-    uint8_t* a3m = nullptr;  // a3's ReLU bitmask (frame-resident path: conv3_fwd_fr writes, conv3_bwd_fr reads)
     float* slab = nullptr;
     size_t slab_floats = 0;
     const float* params = nullptr;  // last synced fp32 params (for biases)
@@ -737,8 +736,8 @@ int conv1_fwd_fr_launch(const uint8_t* frames, const __bf16* w1t, const float* b
                         int nframes, int grid, hipStream_t s);
 int conv2_fwd_fr_launch(const __bf16* a1, const __bf16* w2t, const float* bias, __bf16* a2, int nframes,
                         int grid, hipStream_t s);
-int conv3_fwd_fr_launch(const __bf16* a2, const __bf16* w3t, const float* bias, __bf16* a3, uint8_t* a3m,
-                        int nframes, int grid, hipStream_t s);
+int conv3_fwd_fr_launch(const __bf16* a2, const __bf16* w3t, const float* bias, __bf16* a3, int nframes,
+                        int grid, hipStream_t s);
 int conv12_fwd_fr_launch(const uint8_t* frames, const __bf16* w1t, const float* b1, const __bf16* w2t,
                          const float* b2, __bf16* a1, __bf16* a2, int nframes, int grid, hipStream_t s,
                          int a1_planar);
@@ -749,7 +748,7 @@ int conv21_bwd_fr_launch(const __bf16* a1, const __bf16* da2, const __bf16* w2d,
                          int grid, hipStream_t s, int a1_planar);
 int conv2_bwd_fr_launch(const __bf16* a1, const __bf16* da2, const __bf16* w2d, __bf16* da1, float* slab,
                         float* cs_slab, int nframes, int grid, hipStream_t s);
-int conv3_bwd_fr_launch(const __bf16* a2, const __bf16* da3, const uint8_t* a3m, const __bf16* w3d, __bf16* da2,
+int conv3_bwd_fr_launch(const __bf16* a2, const __bf16* da3, const __bf16* a3, const __bf16* w3d, __bf16* da2,
                         float* slab, float* cs_slab, float* cs2, int nframes, int grid, hipStream_t s);
 
 static AtariImpl* impl(AtariNet* n) { return (AtariImpl*)n->impl; }
@@ -795,7 +794,7 @@ AtariNet* atari_create(int B, int T, int A) {
     bool ok = dmalloc(I, &I->a1, N * 400 * 32) && dmalloc(I, &I->a2, N * 81 * 64) &&
               dmalloc(I, &I->a3, N * 3136) && dmalloc(I, &I->h, N * 512) &&
               dmalloc(I, &I->da1, N * 400 * 32) && dmalloc(I, &I->da2, N * 81 * 64) &&
-              dmalloc(I, &I->da3, N * 3136) && dmalloc(I, &I->dh, N * 512) && dmalloc(I, &I->a3m, N * (3136 / 8)) &&
+              dmalloc(I, &I->da3, N * 3136) && dmalloc(I, &I->dh, N * 512) &&
               dmalloc(I, &I->wb.c1T, 32 * 256) && dmalloc(I, &I->wb.c2T, 64 * 512) &&
               dmalloc(I, &I->wb.c3T, 64 * 576) && dmalloc(I, &I->wb.fcT, (size_t)512 * 3136) &&
               dmalloc(I, &I->wb.hT, 32 * 512) && dmalloc(I, &I->wb.c2D, 4 * 32 * 256) &&
@@ -880,7 +879,7 @@ int atari_forward(AtariNet* n, const uint8_t* frames, float* logits, float* valu
     if (rc) return rc;
     if (I->fr) {
         TagScope ts(tg, "conv3_fwd");
-        rc = conv3_fwd_fr_launch(I->a2, I->wb.c3T, p + o.c3b, I->a3, I->a3m, N, std::min(N, I->fr_grid), s);
+        rc = conv3_fwd_fr_launch(I->a2, I->wb.c3T, p + o.c3b, I->a3, N, std::min(N, I->fr_grid), s);
     } else { TagScope ts(tg, "conv3_fwd"); rc = gemm<128, 64, 2, 2>(ConvGather<9, 64, 3, 1, 7>{I->a2, N * P3}, RowsBf16{I->wb.c3T, C3O, C3K},
                              EpiAct{I->a3, C3O, p + o.c3b, 1.0f}, N * P3, C3O, C3K, s); }
     if (rc) return rc;
@@ -941,7 +940,7 @@ int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, con
         const int grid = std::min(N, I->fr_grid);
         // conv2's bias partials ([grid][2][64] at cs + 3 grid 64, past c3b [grid][64] and
         // c1b [grid][4][32]) come from conv3_bwd (FI_C2B_C3) or from conv21_bwd
-        FI_A("conv3_bwd", conv3_bwd_fr_launch(I->a2, I->da3, I->a3m, I->wb.c3D, I->da2, slab, cs, cs + (size_t)3 * grid * C2O,
+        FI_A("conv3_bwd", conv3_bwd_fr_launch(I->a2, I->da3, I->a3, I->wb.c3D, I->da2, slab, cs, cs + (size_t)3 * grid * C2O,
                                               Nb, grid, s));
         FI_A("reduce_slabs", reduce_slabs(slab, grid, (size_t)C3K * C3O, grads + o.c3w, s));
         FI_A("reduce_slabs", reduce_slabs(cs, grid, (size_t)C3O, grads + o.c3b, s));

@@ -486,12 +486,6 @@ __device__ __forceinline__ int f3_dst(int i) {
 // bordered dY image 203 -> 104).
 __device__ __forceinline__ int rs_lane(int L) { return 8 * (L & 7) + ((2 * (L & 7) + (L >> 3)) & 7); }
 
-// a3's ReLU bitmask (conv_fwd_fr<3> writes it, conv3_bwd_fr reads it): one byte per 16-B
-// unit of a3 (pixel, 8-channel chunk), bit q = channel 8 chunk + q
-namespace c3m {
-constexpr int BYTES = 3136 / 8;  // 392 per frame
-}
-
 template <int L>  // L = 2 (conv2) or 3 (conv3)
 struct FwdGeo;
 template <>
@@ -514,7 +508,6 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
                                                       const __bf16* __restrict__ wt,   // [64][K] (ky,kx,ci)
                                                       const float* __restrict__ bias,  // [64]
                                                       __bf16* __restrict__ y,          // NHWC output frames
-                                                      uint8_t* __restrict__ ymask,     // L == 3: ReLU bitmask (see below)
                                                       int nframes) {
     using G = FwdGeo<L>;
     constexpr int K = G::KS * 32, FPI = G::FPI, STG = G::STG;
@@ -522,13 +515,7 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
     constexpr int NLP = (G::IN_BYTES + 1023) / 1024;   // 1-KiB pieces per input frame
     constexpr int PPW = (NLP + 7) / 8;                  // pieces per wave per frame (at most)
     constexpr int IMG = 2 * FPI * G::XB, SBUF = FPI * NLP * 1024;
-    // L == 3: the iterations' a3 ReLU bitmasks (2 x FPI x 392 B), staged in LDS so that each frame's
-    // 392 bytes leave as one 16-B-per-lane store (one byte store per lane from the epilogue --
-    // partial lines -- cost conv3_fwd 0.17 ms)
-    constexpr int MSTR = 400;  // per-frame stride in LDS (392 rounded up to 16 B: aligned b128 reads)
-    constexpr int MBUF = L == 3 ? 2 * FPI * MSTR : 0;
-    __shared__ __attribute__((aligned(16))) char smem[IMG + STG * SBUF + NLP * 64 * 2 + MBUF];
-    uint8_t* const mbuf = (uint8_t*)(smem + IMG + STG * SBUF + NLP * 64 * 2);
+    __shared__ __attribute__((aligned(16))) char smem[IMG + STG * SBUF + NLP * 64 * 2];
     const int lane = threadIdx.x & 63, tid = threadIdx.x;
     const int w = wave_id(), chh = w >> 2, pg = w & 3;
     const int g = lane >> 4, c16 = lane & 15, si = c16 ^ ((c16 >> 1) & 4);
@@ -632,32 +619,9 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
         }
     };
     constexpr int NSTEP = TPW * G::KS;  // (tile, k-step) steps per iteration
-    // wave u < FPI stores frame u of iteration i2's bitmasks (complete once every wave has passed
-    // the next barrier): lanes 0..24 of one 16-B store, the descriptor's 392-B range drops the
-    // rest. The LDS read happens right after that barrier, the store after the MFMA pipeline.
-    auto load_masks = [&](int i2) {
-        return *(const u32x4*)(mbuf + ((i2 & 1) * FPI + min(w, FPI - 1)) * MSTR + 16 * min(lane, 24));
-    };
-    auto store_masks = [&](int i2, const u32x4& v) {
-        int n = 0;
-        if constexpr (L == 3) {
-            const int k = FPI * i2 + w;
-            if (w < FPI && k < nmine) {
-                const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-                    ymask + (size_t)(blockIdx.x + k * gridDim.x) * c3m::BYTES, 0, c3m::BYTES, 0x00020000);
-                __builtin_amdgcn_raw_buffer_store_b128(v, r, 16 * lane, 0, 0);
-                ++n;
-            }
-        }
-        return n;
-    };
     for (int it = 0; it < niter; ++it) {
         const char* X = smem + (it & 1) * FPI * G::XB;
         lds_barrier();  // iteration it's image written; iteration it-1 consumed by every wave
-        u32x4 mprev = u32x4{0, 0, 0, 0};
-        if constexpr (L == 3) {
-            if (it > 0 && w < FPI) mprev = load_masks(it - 1);
-        }
         // tile-outer steps: each tile's 2*KS MFMAs end in its 16-byte store; B fragments are
         // read PD steps ahead of their MFMAs
         constexpr int PD = 4;
@@ -666,10 +630,6 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
         for (int st = 0; st < PD; ++st) fb[st] = *(const bf16x8*)(X + bbase[st / G::KS] + imm(st % G::KS));
         __builtin_amdgcn_sched_group_barrier(0x100, PD, 0);
         f32x4 acc0 = f32x4{}, acc1 = f32x4{};
-        uint32_t mreg[TPW];  // L == 3: tile i's unit << 8 | frame << 24 | valid << 31
-        u32x4 vreg[TPW];     // ... and its 8 stored a3 values
-#pragma unroll
-        for (int i = 0; i < TPW; ++i) mreg[i] = 0;
 #pragma unroll
         for (int st = 0; st < NSTEP; ++st) {
             const int i = st / G::KS, ks = st % G::KS;
@@ -694,40 +654,12 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
                             ov[4 + r] = (__bf16)fmaxf(acc1[r] + bch[4 + r], 0.f);
                         }
                         u32x4* dst = (u32x4*)(y + (size_t)(blockIdx.x + k * gridDim.x) * G::OUT_ELEMS);
-                        const int unit = 8 * (G::OW * oy + ox) + 4 * chh + g;
-                        FI_ST16(__builtin_bit_cast(u32x4, ov), dst + unit);
-                        if constexpr (L == 3) {
-                            // kept for the bitmask, which is built after the MFMA pipeline (an LDS
-                            // write here, inside the prefetched B-fragment pipeline, cost
-                            // conv3_fwd 0.16 ms)
-                            vreg[i] = __builtin_bit_cast(u32x4, ov);
-                            mreg[i] = (uint32_t)unit << 8 | (uint32_t)fi << 24 | 1u << 31;
-                        }
+                        FI_ST16(__builtin_bit_cast(u32x4, ov), dst + 8 * (G::OW * oy + ox) + 4 * chh + g);
                     }
                 }
                 acc0 = f32x4{};
                 acc1 = f32x4{};
             }
-        }
-        if constexpr (L == 3) {
-            // this iteration's mask bytes into LDS, after the MFMA pipeline. conv3_bwd_fr needs a3
-            // only as the ReLU mask of da3: bit q of byte `unit` = (a3 element 8 unit + q > 0), the
-            // predicate it applied to the stored bf16 (392 B per frame instead of re-reading
-            // 6,272 B of a3). 0 - x with i16 saturation is negative exactly for x > 0: the sign
-            // bits of one v_pk_sub_i16 per pair are the pair's two mask bits
-#pragma unroll
-            for (int i = 0; i < TPW; ++i)
-                if (mreg[i] >> 31) {
-                    uint32_t m = 0;
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        uint32_t t;
-                        asm("v_pk_sub_i16 %0, 0, %1 clamp" : "=v"(t) : "v"(vreg[i][j]));
-                        m |= ((t >> 15) & 1u) << (2 * j) | ((t >> 31) & 1u) << (2 * j + 1);
-                    }
-                    mbuf[((it & 1) * FPI + ((mreg[i] >> 24) & 0x7f)) * MSTR + ((mreg[i] >> 8) & 0xffff)] = (uint8_t)m;
-                }
-            if (it > 0) issued += store_masks(it - 1, mprev);
         }
         if (it + 1 < niter) {
             wait_vmcnt(issued - mk[0]);  // own pieces of iteration it + 1 landed (stores may fly)
@@ -742,26 +674,19 @@ __global__ __launch_bounds__(512, 2) void conv_fwd_fr(const __bf16* __restrict__
         for (int q = 0; q + 1 < STG; ++q) mk[q] = mk[q + 1];
         mk[STG - 1] = mnew;
     }
-    if constexpr (L == 3) {
-        if (niter > 0) {
-            __syncthreads();  // the last iteration's bitmask bytes written by every wave
-            if (w < FPI) store_masks(niter - 1, load_masks(niter - 1));
-        }
-    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 int conv2_fwd_fr_launch(const __bf16* a1, const __bf16* w2t, const float* bias, __bf16* a2, int nframes,
                         int grid, hipStream_t s) {
-    hipLaunchKernelGGL(conv_fwd_fr<2>, dim3(grid), dim3(512), 0, s, a1, w2t, bias, a2, (uint8_t*)nullptr, nframes);
+    hipLaunchKernelGGL(conv_fwd_fr<2>, dim3(grid), dim3(512), 0, s, a1, w2t, bias, a2, nframes);
     FI_HIP_CHECK(hipGetLastError());
     return FI_OK;
 }
 
-int conv3_fwd_fr_launch(const __bf16* a2, const __bf16* w3t, const float* bias, __bf16* a3, uint8_t* a3m,
-                        int nframes, int grid, hipStream_t s) {
-    FI_REQUIRE(a3m != nullptr, "conv3_fwd_fr: the a3 ReLU bitmask buffer is required");
-    hipLaunchKernelGGL(conv_fwd_fr<3>, dim3(grid), dim3(512), 0, s, a2, w3t, bias, a3, a3m, nframes);
+int conv3_fwd_fr_launch(const __bf16* a2, const __bf16* w3t, const float* bias, __bf16* a3, int nframes,
+                        int grid, hipStream_t s) {
+    hipLaunchKernelGGL(conv_fwd_fr<3>, dim3(grid), dim3(512), 0, s, a2, w3t, bias, a3, nframes);
     FI_HIP_CHECK(hipGetLastError());
     return FI_OK;
 }
@@ -1741,31 +1666,27 @@ __host__ __device__ constexpr int zc(int c) { return 8 * (c & 1) + 4 * ((c >> 1)
 }  // namespace c3
 
 struct C3Ctx {
-    const __bf16 *a2, *da3;
-    const uint8_t* a3m;  // a3's ReLU bitmask (c3m)
+    const __bf16 *a2, *da3, *a3;
     __bf16* da2;
     int nframes;
 };
 
-// Linear-DMA pipeline: every frame's a2, da3 and a3's ReLU bitmask arrive by LDS-DMA in their
-// own byte order (1 KiB contiguous per wave instruction) into one of two staging buffers; the
-// issuing wave then moves its own landed pieces into the frame's image slot (chunk-planar X,
-// bordered dY), applying the a3 mask to da3 on the way, so the mask image needs no slot. (Round
-// 5: the mask is conv_fwd_fr<3>'s 392-byte bitmask, one piece per issuing wave, instead of a3
-// itself, 7 pieces / 6,272 B per frame.) The gathered
+// Linear-DMA pipeline: every frame's a2, da3 and a3 arrive by LDS-DMA in their own byte order
+// (1 KiB contiguous per wave instruction) into one of two staging buffers; the issuing wave
+// then moves its own landed pieces into the frame's image slot (chunk-planar X, bordered dY),
+// applying the a3 ReLU mask to da3 on the way, so the mask image needs no slot. The gathered
 // DMA straight into the image layouts issued 16-byte pieces at a 128-byte
 // stride: the same bytes, 8x the memory requests (timing with linear sources and wrong
 // layouts: 4.29 -> 3.85 ms; the gathered form is no longer built).
 // LDS: 2 image slots (X + dY, 28,672 B each; gap / border units zeroed once, never written),
-// 2 staging buffers (a2 11 + da3 7 + 4 bitmask copies, pieces of 1 KiB), destination tables:
-// 104,480 B.
+// 2 staging buffers (a2 11 + da3 7 + a3 7 pieces of 1 KiB), destination tables: 110,624 B.
 namespace c3 {
 constexpr int SLOT2 = XB + DYB;                    // 28,672
-constexpr int NPX = 11, NPD = 7;                   // 1-KiB pieces of a2, of da3
-constexpr int STGB = (NPX + NPD + 4) * 1024;       // 22,528 (+ the a3 bitmask, one copy per issuing wave)
+constexpr int NPX = 11, NPD = 7;                   // 1-KiB pieces of a2, of da3 (= of a3)
+constexpr int STGB = (NPX + 2 * NPD) * 1024;       // 25,600
 constexpr int NUX = 10368 / 16, NUD = 6272 / 16;   // 16-B units of a2, of da3
 constexpr int O_STG = 2 * SLOT2, O_TAB = O_STG + 2 * STGB;
-constexpr int LDS = O_TAB + (NUX + NUD) * 2;       // 104,480
+constexpr int LDS = O_TAB + (NUX + NUD) * 2;       // 110,624
 }  // namespace c3
 
 // ISSUER: waves 0-3 (compile-time role, so the data-gradient waves carry none of the DMA /
@@ -1791,7 +1712,7 @@ __device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, int nst, W
         const int f = blockIdx.x + k * gridDim.x;
         const fi_i32x4 xr = make_rsrc(c.a2 + (size_t)f * 5184, 10368);
         const fi_i32x4 dr = make_rsrc(c.da3 + (size_t)f * 3136, 6272);
-        const fi_i32x4 mr = make_rsrc(c.a3m + (size_t)f * c3m::BYTES, c3m::BYTES);
+        const fi_i32x4 mr = make_rsrc(c.a3 + (size_t)f * 3136, 6272);
         const uint32_t base = lds0 + c3::O_STG + sb * c3::STGB;
         int n = 0;
 #pragma unroll
@@ -1807,14 +1728,11 @@ __device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, int nst, W
             const int j = w + 4 * i;
             if (j < c3::NPD) {
                 blds16(dr, 1024 * j + 16 * lane, base + 1024 * (c3::NPX + j));
-                ++n;
+                blds16(mr, 1024 * j + 16 * lane, base + 1024 * (c3::NPX + c3::NPD + j));
+                n += 2;
             }
         }
-        // the whole bitmask (392 B; lanes past it read zeros) into this wave's own copy: the
-        // reshuffle below runs right after the wave's OWN vmcnt wait, so it may only read pieces
-        // this wave issued (one shared copy from one wave raced the other waves' reads)
-        blds16(mr, 16 * lane, base + 1024 * (c3::NPX + c3::NPD + w));
-        return n + 1;
+        return n;
     };
     const int sl = rs_lane(lane);  // lane order with bank-conflict-free write groups
     auto reshuffle = [&](int sb, int slot) {  // own landed pieces -> image slot (a2, then da3: reads, then writes)
@@ -1833,14 +1751,13 @@ __device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, int nst, W
             for (int i = 0; i < 3; ++i)
                 if (64 * (w + 4 * i) + sl < c3::NUX) *(u32x4*)(im + 16 * xd[i]) = xv[i];
         }
-        s16x8 dv[2];
-        uint32_t mb[2];
+        s16x8 dv[2], mv[2];
         int dd[2];
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int u = min(64 * (w + 4 * i) + sl, c3::NUD - 1);
             dv[i] = *(const s16x8*)(st + 1024 * c3::NPX + 16 * u);
-            mb[i] = *(const uint8_t*)(st + 1024 * (c3::NPX + c3::NPD + w) + u);
+            mv[i] = *(const s16x8*)(st + 1024 * (c3::NPX + c3::NPD) + 16 * u);
             dd[i] = dsty[u];
         }
 #pragma unroll
@@ -1848,7 +1765,7 @@ __device__ __forceinline__ void c3_frames(const C3Ctx& c, char* smem, int nst, W
             if (64 * (w + 4 * i) + sl < c3::NUD) {
                 s16x8 v = dv[i];
 #pragma unroll
-                for (int q = 0; q < 8; ++q) v[q] = (mb[i] >> q) & 1u ? v[q] : (short)0;
+                for (int q = 0; q < 8; ++q) v[q] = mv[i][q] > 0 ? v[q] : (short)0;
                 *(s16x8*)(im + c3::XB + 16 * dd[i]) = v;
             }
     };
@@ -1964,7 +1881,7 @@ __device__ __forceinline__ void c3_wgrad(const C3Ctx& ctx, char* smem, float* sl
 
 __global__ __launch_bounds__(512, 2) void conv3_bwd_fr(const __bf16* __restrict__ a2,
                                                        const __bf16* __restrict__ da3,  // unmasked
-                                                       const uint8_t* __restrict__ a3m,  // its mask (c3m)
+                                                       const __bf16* __restrict__ a3,   // its mask
                                                        const __bf16* __restrict__ w3d,  // [64 ci][576]
                                                        __bf16* __restrict__ da2,
                                                        float* __restrict__ slab,     // [grid][576][64]
@@ -1975,7 +1892,7 @@ __global__ __launch_bounds__(512, 2) void conv3_bwd_fr(const __bf16* __restrict_
     const int lane = threadIdx.x & 63;
     const int w = wave_id(), wr = w & 3;
     const int g = lane >> 4;
-    const C3Ctx ctx{a2, da3, a3m, da2, nframes};
+    const C3Ctx ctx{a2, da3, a3, da2, nframes};
 
     if (w < 4) {
         if (wr >> 1) c3_wgrad<1>(ctx, smem, slab, cs_slab, wr);
@@ -2084,10 +2001,9 @@ __global__ __launch_bounds__(512, 2) void conv3_bwd_fr(const __bf16* __restrict_
     }
 }
 
-int conv3_bwd_fr_launch(const __bf16* a2, const __bf16* da3, const uint8_t* a3m, const __bf16* w3d, __bf16* da2,
+int conv3_bwd_fr_launch(const __bf16* a2, const __bf16* da3, const __bf16* a3, const __bf16* w3d, __bf16* da2,
                         float* slab, float* cs_slab, float* cs2, int nframes, int grid, hipStream_t s) {
-    FI_REQUIRE(a3m != nullptr, "conv3_bwd_fr: the a3 ReLU bitmask is required");
-    hipLaunchKernelGGL(conv3_bwd_fr, dim3(grid), dim3(512), 0, s, a2, da3, a3m, w3d, da2,
+    hipLaunchKernelGGL(conv3_bwd_fr, dim3(grid), dim3(512), 0, s, a2, da3, a3, w3d, da2,
                        slab, cs_slab, cs2, nframes);
     FI_HIP_CHECK(hipGetLastError());
     return FI_OK;
