@@ -82,3 +82,32 @@ def test_config5_shape_mpi_end_to_end_vs_oracle(orc, tmp_path):
     latest = np.fromfile(ck / "model_0_latest.bin", np.uint8)
     assert int(latest[:8].view(np.uint64)[0]) == 4
     np.testing.assert_array_equal(latest[8:].view(np.float32), p)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_config5_64_actor_ranks_end_to_end(orc, tmp_path):
+    """BASELINE config #5's rank count: 64 MPI actor ranks on the host cores feeding the device
+    learner on rank 0 (one GPU here; the 8-GPU form needs an 8-GPU node). 64 x 16 trajectories
+    of T = 100 (105 MB) through the rank-0 receiver into the SharedBuffer; the learner runs
+    floor(64 * 16 / 256) = 4 iterations at M = 256. Every message arrives once and intact, every
+    actor's version request is answered, weight replies carry whole blobs, and the first consumed batch is replayed through the
+    oracle (SGD: its published parameter difference / lr is the gradient)."""
+    T, B, A, D, H, lr, actors, iters = 100, 256, 18, 128, 256, 1e-3, 64, 16
+    dump = tmp_path / "dump"
+    args = ["--players", "1", "--iterations", str(iters), "--buffer-capacity", str(2 * B), "--batch-size", str(B),
+            "--seq-length", str(T), "--entry-size", str(T + 1), "--game-steps", str(T + 1), "--agent-time", "0",
+            "--checkpoint-freq", "0", "--checkpoint-location", str(tmp_path / "ck"), "--optimizer", "sgd",
+            "--lr", str(lr), "--max-grad-norm", "0", "--seed", "5", "--dump-dir", str(dump), "--log-level", "warn"]
+    r = mpirun(actors + 1, [EXE] + args, timeout=280)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["expected_iterations"] == actors * iters // B and out["learner_iterations"] == [actors * iters // B]
+    m = out["mpi"]
+    assert m["actors"] == actors and m["trajectories"] == actors * iters and m["bad_messages"] == 0
+    assert m["trajectory_bytes"] == actors * iters * (T + 1) * 1024
+    assert m["version_requests"] == actors * iters
+    assert m["weights_bytes"] == m["weights_replies"] * (8 + out["param_bytes"])
+    assert out["metrics"]["rejected_batches"] == 0
+    p = np.fromfile(dump / "params_0_0.bin", np.float32)
+    assert_step_matches_oracle(orc, dump, 0, p, T, B, A, D, H, lr)
