@@ -699,32 +699,41 @@ int conv3_fwd_fr_launch(const __bf16* a2, const __bf16* w3t, const float* bias, 
 //     result goes to HBM at once and is HELD in registers until the next iteration writes it
 //     into the conv2 input image (conv_fwd_fr<2>'s chunk-planar class-plane layout);
 //   waves 4-7 (conv2 role): conv2 of the PREVIOUS frame from that image as conv_fwd_fr<2>
-//     (W2 channel half chh in registers, s-grid tiles 3pg..3pg+2), and all raw-frame DMA.
-// Iteration it: [B1] all 8 waves convert raw(it) into the bf16 pair-plane image, the conv1
-// waves also write a1(it-1) into the conv2 image  [B2]  conv1(it) MFMAs on waves 0-3 beside
-// conv2(it-1) MFMAs on waves 4-7 (sharing each SIMD's matrix pipe), raw(it+2) DMA'd into the
-// slot converted in this iteration.
-// LDS: 2 raw slots (57,344) + conv1 image (56,576) + conv2 image (26,880) = 140,800 B.
+//     (W2 channel half chh in registers, s-grid tiles 3pg..3pg+2).
+// The u8 -> bf16 conversion of frame it+1 overlaps frame it: two conv1 images (frame it is read
+// by the conv1 MFMAs while frame it+1 is written), the raw bytes by plain 16-byte loads into
+// registers one frame ahead, each unit's register reloaded right after its conversion.
+// Iteration it: [B1] phase A: the conv1 role writes a1(it-1) into the conv2 image and converts
+// NCA units per lane of raw(it+1); the conv2 role converts NA units per lane  [B2] phase B:
+// conv1(it) MFMAs on waves 0-3 beside conv2(it-1) MFMAs on waves 4-7 (sharing each SIMD's
+// matrix pipe), the conv1 role converting its remaining NC - NCA units between its tiles.
+// (Round 5; before, two raw LDS-DMA slots and one image: the whole conversion in a phase of its
+// own, 1.4k clocks per frame without MFMAs. Measured splits, conv12_fwd ms vs 5.86-6.02 for the
+// old kernel in the same runs (scripts/r05_gpu_batch.sh, profiles/r05_conv12_split_ab.txt):
+// NCA/NC/NA/NB = 1/3/4/0 5.65-5.75 (kept), 2/3/4/0 5.69-5.76, 0/3/4/0 5.70-5.80, 3/3/4/0
+// 5.77-5.86, 0/2/3/2 5.81-5.83, 0/3/3/1 5.71-5.80, 0/2/2/3 6.54-6.56: units converted between
+// the conv2 MFMAs (NB) cost ~650 clocks each, between the conv1 MFMAs ~390, in phase A ~300;
+// raw units DMA'd into an LDS staging area instead of registers 6.03-6.07; s_setprio 1 on
+// either role neutral / +0.15 ms.)
+// LDS: 2 conv1 images (113,152) + conv2 image (26,880) = 140,032 B.
 // HBM per frame: 28,224 (frame) + 25,600 (a1) + 10,368 (a2) = 64,192 B (vs 89,792 B for the
 // two kernels separately).
 // =====================================================================================
 namespace c12 {
-constexpr int X2 = 1680 * 16;  // conv2 input image (FwdGeo<2>::XB)
-constexpr int LDS = 2 * c1::RAW + c1::IMG + X2;
+constexpr int X2 = 1680 * 16;             // conv2 input image (FwdGeo<2>::XB)
+constexpr int LDS = 2 * c1::IMG + X2;     // 140,032 B
+// raw units per lane: NC by the conv1 role (units tid + 256i; the first NCA in phase A), NA by
+// the conv2 role (units 256 NC + t4 + 256i) in phase A
+constexpr int NCA = 1, NC = 3, NA = 4;
+static_assert(256 * (NC + NA) >= c1::FRAME_LOADS && 256 * (NC + NA - 1) < c1::FRAME_LOADS, "units");
+static_assert(NCA <= NC && NC <= 6, "conv1-role units: one per tile");
 }  // namespace c12
 
-// all 512 threads: raw u8 frame (LDS) -> bf16 pair-plane conv1 image
-__device__ __forceinline__ void c12_convert(const char* raw, char* img, int tid) {
-#pragma unroll
-    for (int i = 0; i < (c1::FRAME_LOADS + 511) / 512; ++i) {
-        const int u = tid + 512 * i;
-        if (u < c1::FRAME_LOADS) {
-            bf16x8 lo, hi;
-            u8x16_to_bf16(*(const u32x4*)(raw + 16 * u), lo, hi);
-            *(bf16x8*)(img + 16 * u) = lo;
-            *(bf16x8*)(img + c1::PLANE + 16 * u) = hi;
-        }
-    }
+__device__ __forceinline__ void c12_cvt_unit(u32x4 v, char* img, int u) {
+    bf16x8 lo, hi;
+    u8x16_to_bf16(v, lo, hi);
+    *(bf16x8*)(img + 16 * u) = lo;
+    *(bf16x8*)(img + c1::PLANE + 16 * u) = hi;
 }
 
 __global__ __launch_bounds__(512, 2) void conv12_fwd_fr(const uint8_t* __restrict__ frames,
@@ -735,12 +744,13 @@ __global__ __launch_bounds__(512, 2) void conv12_fwd_fr(const uint8_t* __restric
                                                         __bf16* __restrict__ a1, __bf16* __restrict__ a2,
                                                         int nframes, int a1_planar) {
     __shared__ __attribute__((aligned(16))) char smem[c12::LDS];
-    char* img = smem + 2 * c1::RAW;
-    char* x2 = img + c1::IMG;
+    char* x2 = smem + 2 * c1::IMG;
     const int lane = threadIdx.x & 63, tid = threadIdx.x, w = wave_id();
     const int g = lane >> 4, c16 = lane & 15, si = c16 ^ ((c16 >> 1) & 4);
     for (int i = tid; i < c12::X2 / 16; i += 512) ((u32x4*)x2)[i] = u32x4{0, 0, 0, 0};  // gap units
     const int nmine = nframes > (int)blockIdx.x ? (nframes - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+    auto raw_of = [&](int k) { return (const u32x4*)(frames + (size_t)(blockIdx.x + k * gridDim.x) * 28224); };
+    auto img_of = [&](int k) { return smem + (k & 1) * c1::IMG; };
 
     if (w < 4) {
         // ---------------- conv1 role
@@ -756,17 +766,45 @@ __global__ __launch_bounds__(512, 2) void conv12_fwd_fr(const uint8_t* __restric
         const float inv255 = 1.0f / 255.0f;
         const int ntile = w == 0 ? 7 : 6;  // tiles w + 4tt < 25
         u32x4 held[7];                     // a1 of the previous frame, tile tt
+        u32x4 rr[c12::NC];                 // raw units tid + 256i of the next frame to convert
+        if (nmine > 0) {
+            const u32x4* src = raw_of(0);
+#pragma unroll
+            for (int i = 0; i < c12::NC; ++i) rr[i] = src[tid + 256 * i];
+#pragma unroll
+            for (int i = 0; i < c12::NC; ++i) c12_cvt_unit(rr[i], img_of(0), tid + 256 * i);
+        }
+        if (nmine > 1) {
+            const u32x4* src = raw_of(1);
+#pragma unroll
+            for (int i = 0; i < c12::NC; ++i) rr[i] = src[tid + 256 * i];
+        }
+        // every prologue load landed: the compiler's waits in the frame loop then follow only the
+        // loop's own loads (it merges the preheader's pending loads into the loop head otherwise and
+        // waits for all of them, stores included, in every frame). The builtin, not asm: the
+        // compiler's wait pass reads it
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
         for (int it = 0; it <= nmine; ++it) {
             const int f = blockIdx.x + it * gridDim.x;
-            lds_barrier();  // B1: raw(it) landed (waited by its issuers); conv1 image and a1 image free
+            const bool cvt = it + 1 < nmine, rel = it + 2 < nmine;  // convert raw(it+1); reload for it+2
+            const u32x4* nsrc = raw_of(rel ? it + 2 : it);
+            char* nimg = img_of(it + 1);
+            lds_barrier();  // B1: image(it) complete; the conv2 image read by conv2(it-2)
             if (it >= 1) {  // a1(it-1) -> conv2 image (pixel q, chunk g)
 #pragma unroll
                 for (int tt = 0; tt < 7; ++tt)
                     if (tt < ntile) *(u32x4*)(x2 + 16 * f2_dst(4 * ((w + 4 * tt) * 16 + si) + g)) = held[tt];
             }
-            if (it < nmine) c12_convert(smem + (it & 1) * c1::RAW, img, tid);
-            lds_barrier();  // B2: conv1 image and conv2 image complete
+            if (cvt) {
+#pragma unroll
+                for (int i = 0; i < c12::NCA; ++i) {
+                    c12_cvt_unit(rr[i], nimg, tid + 256 * i);
+                    if (rel) rr[i] = nsrc[tid + 256 * i];
+                }
+            }
+            lds_barrier();  // B2: the conv2 image complete
             if (it < nmine) {
+                const char* img = img_of(it);
                 u32x4* dst = (u32x4*)(a1 + (size_t)f * 12800);
                 auto load = [&](int t, bf16x8* d) {
                     const int q = t * 16 + si, oy = q / 20, ox = q - 20 * oy;
@@ -789,10 +827,16 @@ __global__ __launch_bounds__(512, 2) void conv12_fwd_fr(const uint8_t* __restric
                             da = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[0][ks], cur[ks], da, 0, 0, 0);
                             db = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[1][ks], cur[ks], db, 0, 0, 0);
                         }
+                        const bool unit_here = tt >= c12::NCA && tt < c12::NC;  // tile tt converts unit tt
+                        if (unit_here && cvt) {
+                            c12_cvt_unit(rr[tt], nimg, tid + 256 * tt);
+                            if (rel) rr[tt] = nsrc[tid + 256 * tt];
+                        }
 #pragma unroll
                         for (int ks = 0; ks < 8; ++ks) {
                             __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
                             if (tt + 1 < ntile) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                            if (unit_here) __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
                         }
                         bf16x8 o;
 #pragma unroll
@@ -814,9 +858,8 @@ __global__ __launch_bounds__(512, 2) void conv12_fwd_fr(const uint8_t* __restric
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
-        // ---------------- conv2 role (+ raw-frame DMA)
-        const int wr = w - 4, chh = wr & 1, pg = wr >> 1;
-        const uint32_t lds0 = lds_addr(smem);
+        // ---------------- conv2 role
+        const int wr = w - 4, chh = wr & 1, pg = wr >> 1, t4 = tid - 256;
         bf16x8 wa[2][16];  // lane holds W2[co = 32chh + 8(i>>2) + 4ct + (i&3), i = c16][k = 32ks + 8g..+8]
 #pragma unroll
         for (int ct = 0; ct < 2; ++ct)
@@ -834,32 +877,39 @@ __global__ __launch_bounds__(512, 2) void conv12_fwd_fr(const uint8_t* __restric
             const int ky = ks >> 2, kx = ks & 3;
             return 16 * (10 * (ky >> 1) + (kx >> 1) + 100 * (2 * (ky & 1) + (kx & 1)));
         };
-        // raw frame k: pieces j = wr + 4i (7 per wave, 28 KiB; bytes past the frame read as 0)
-        auto issue_raw = [&](int k, int slot) {
-            const fi_i32x4 rr = make_rsrc(frames + (size_t)(blockIdx.x + k * gridDim.x) * 28224, 28224);
+        auto unit = [&](int i) { return 256 * c12::NC + t4 + 256 * i; };
+        auto valid = [&](int i) { return i + 1 < c12::NA || unit(i) < c1::FRAME_LOADS; };
+        u32x4 rr[c12::NA];
+        if (nmine > 0) {
+            const u32x4* src = raw_of(0);
 #pragma unroll
-            for (int i = 0; i < 7; ++i) {
-                const int j = wr + 4 * i;
-                blds16(rr, 16 * lane + 1024 * j, lds0 + slot * c1::RAW + 1024 * j);
-            }
-            return 7;
-        };
-        // issue order: raw(0) raw(1) | per iteration: raw(it+2), then conv2(it-1)'s 3 stores
-        int issued = 0, m0 = 0, m1 = 0;
-        if (nmine > 0) issued += issue_raw(0, 0);
-        m0 = issued;
-        if (nmine > 1) issued += issue_raw(1, 1);
-        m1 = issued;
+            for (int i = 0; i < c12::NA; ++i)
+                if (valid(i)) rr[i] = src[unit(i)];
+#pragma unroll
+            for (int i = 0; i < c12::NA; ++i)
+                if (valid(i)) c12_cvt_unit(rr[i], img_of(0), unit(i));
+        }
+        if (nmine > 1) {
+            const u32x4* src = raw_of(1);
+#pragma unroll
+            for (int i = 0; i < c12::NA; ++i)
+                if (valid(i)) rr[i] = src[unit(i)];
+        }
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), as the conv1 role
         for (int it = 0; it <= nmine; ++it) {
-            if (it < nmine) wait_vmcnt(issued - m0);  // own pieces of raw(it) landed
             lds_barrier();  // B1
-            if (it < nmine) c12_convert(smem + (it & 1) * c1::RAW, img, tid);
-            lds_barrier();  // B2: raw slot it&1 converted; a1(it-1) in the conv2 image
-            int m2 = issued;
-            if (it + 2 < nmine) {
-                issued += issue_raw(it + 2, it & 1);
-                m2 = issued;
+            if (it + 1 < nmine) {  // raw(it+1) -> the next image (free since B1)
+                const bool rel = it + 2 < nmine;
+                const u32x4* nsrc = raw_of(rel ? it + 2 : it);
+#pragma unroll
+                for (int i = 0; i < c12::NA; ++i) {
+                    if (valid(i)) {
+                        c12_cvt_unit(rr[i], img_of(it + 1), unit(i));
+                        if (rel) rr[i] = nsrc[unit(i)];
+                    }
+                }
             }
+            lds_barrier();  // B2: a1(it-1) in the conv2 image
             if (it >= 1) {  // conv2 of frame it-1 from the a1 image
                 const int k = it - 1;
                 u32x4* dst = (u32x4*)(a2 + (size_t)(blockIdx.x + k * gridDim.x) * 5184);
@@ -894,10 +944,7 @@ __global__ __launch_bounds__(512, 2) void conv12_fwd_fr(const uint8_t* __restric
                         acc1 = f32x4{};
                     }
                 }
-                issued += 3;  // every tile has valid pixels: three store instructions
             }
-            m0 = m1;
-            m1 = m2;
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }

@@ -171,8 +171,9 @@ __device__ __forceinline__ int nt_chunk(int c, int row) {
 // 4 = accumulators in AGPRs (for 4-wave tiles of 128 x 128 per wave), 8 = non-temporal loads of
 // the Y operand (the frame rows), 16 = the next step's DMA issued after the first sub-step's
 // fragment reads (their LDS latency overlaps the issue), 32 = ... after the first sub-step's MFMAs,
-// 64 = LDS-read prefetch across the barrier (BK 32, NS >= 4; see the branch below), 4096 = one
-// barrier per step, between its two halves (BK 64, NS 2; see the branch below)
+// 64 = LDS-read prefetch across the barrier (BK 32, NS >= 4; see the branch below), 128 = tile
+// rows dealt to XCDs in contiguous eighths (tile_of below), 4096 = one barrier per step, between
+// its two halves (BK 64, NS 2; see the branch below)
 template <int BX, int BY, int WX, int WY, int BK, int NS, class Epi, int OPT = 0>
 __global__ __launch_bounds__(64 * WX * WY) void fc_nt_kernel(const __bf16* __restrict__ X, const __bf16* __restrict__ Y,
                                                     int NY, int K, int ntx, int ntiles, Epi epi) {
@@ -192,14 +193,23 @@ __global__ __launch_bounds__(64 * WX * WY) void fc_nt_kernel(const __bf16* __res
     const int wx = w / WY, wy = w % WY;
     const int NG = gridDim.x, lg = xcd_remap(blockIdx.x, NG);
     const int nk = K / BK;
-    const int total = ((ntiles - 1 - lg) / NG + 1) * nk;
+    // tile i of this workgroup. Default: lg + i NG (the XCD-contiguous lg of xcd_remap). OPT 128:
+    // each XCD owns a contiguous eighth of the tile ROWS (ty) and its NG / 8 workgroups walk it
+    // tile by tile, so the ntx tiles of a row -- which share its Y rows -- run on one XCD at
+    // about the same time (with lg, a row's tiles straddle two XCDs at every 32-tile boundary)
+    const bool xrow = (OPT & 128) && NG % 8 == 0;
+    const int xcd = blockIdx.x % 8, jx = blockIdx.x / 8, ngx = NG / 8;
+    const int nty_ = ntiles / ntx, r0x = xcd * nty_ / 8, r1x = (xcd + 1) * nty_ / 8;
+    const int nmy = xrow ? ((r1x - r0x) * ntx - jx + ngx - 1) / ngx : (ntiles - 1 - lg) / NG + 1;
+    auto tile_of = [&](int i) { return xrow ? r0x * ntx + jx + i * ngx : lg + i * NG; };
+    const int total = max(nmy, 0) * nk;
     const uint32_t lbase = lds_addr(lds);
     const float* lb = (const float*)(lds + NS * SLOT);
     epi.init((float*)(lds + NS * SLOT), threadIdx.x, 64 * NW);
 
     int is_tile = 0, is_kt = 0;  // the next step to issue (tile index of this workgroup, k-step)
     auto issue = [&](int it) {   // this wave's 1-KiB pieces of step `it` into slot it % NS
-        const int t = lg + is_tile * NG;
+        const int t = tile_of(is_tile);
         const int ty = t / ntx, tx = t - ty * ntx;
         const int x0 = tx * BX, y0 = ty * BY;
         const fi_i32x4 rx = make_rsrc(X + (size_t)x0 * K, (uint32_t)BX * K * 2);
@@ -278,7 +288,7 @@ __global__ __launch_bounds__(64 * WX * WY) void fc_nt_kernel(const __bf16* __res
 #pragma unroll
                 for (int g = 0; g < FY; ++g) cb[g] = nb[g];
             }
-            const int t = lg + tile_it * NG;
+            const int t = tile_of(tile_it);
             const int ty = t / ntx, tx = t - ty * ntx;
             const int y0 = ty * BY;
             const OutTile ot = epi.tile(y0, min(BY, NY - y0));
@@ -359,7 +369,7 @@ __global__ __launch_bounds__(64 * WX * WY) void fc_nt_kernel(const __bf16* __res
                         acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ha[f], hb[g], acc[f][g], 0, 0, 0);
                 if constexpr (OPT & 1) __builtin_amdgcn_s_setprio(0);
             }
-            const int t = lg + tile_it * NG;
+            const int t = tile_of(tile_it);
             const int ty = t / ntx, tx = t - ty * ntx;
             const int y0 = ty * BY;
             const OutTile ot = epi.tile(y0, min(BY, NY - y0));
@@ -427,7 +437,7 @@ __global__ __launch_bounds__(64 * WX * WY) void fc_nt_kernel(const __bf16* __res
                 }
             }
         }
-        const int t = lg + tile_it * NG;
+        const int t = tile_of(tile_it);
         const int ty = t / ntx, tx = t - ty * ntx;
         const int y0 = ty * BY;
         const OutTile ot = epi.tile(y0, min(BY, NY - y0));
@@ -570,8 +580,11 @@ __global__ __launch_bounds__(512) void fc_tn_kernel(const __bf16* __restrict__ X
 // step between its two halves, non-temporal frame loads (round 4: 1.257 -> 1.17-1.20 ms)
 #define FC_FW_CFG 256, 256, 4, 2, 64, 2, 8 | 4096
 // dgrad: 3136 = 14 x 224 output columns, 256 rows, waves 1 x 8 (14 x 2 fragments per wave),
-// s_setprio, non-temporal da3 stores (round 4: 1.652 -> 1.591 ms)
-#define FC_DG_CFG 224, 256, 1, 8, 64, 2, 1 | 2
+// s_setprio, non-temporal da3 stores (round 4: 1.652 -> 1.591 ms), tile rows dealt to XCDs in
+// contiguous eighths so a row's 14 tiles share one XCD's L2 (round 5: 1.60-1.65 -> 1.56-1.60 ms
+// alone, 1.69 -> 1.64 ms in the step; 4.47 -> 3.96 GB of HBM traffic per launch; with default
+// stores 1.535-1.57 ms but 6.4 GB: the partial-line da3 writes are fetched first)
+#define FC_DG_CFG 224, 256, 1, 8, 64, 2, 1 | 2 | 128
 // wgrad: x = dh columns (2 x 256), y = a3 columns (14 x 224), waves 4 x 2
 #define FC_WG_CFG 256, 224, 4, 2, 64, 2
 #endif

@@ -5,7 +5,7 @@
 // Build: scripts/build_fc_bench.sh; run: build/fc_bench [rounds]
 #define FI_FC_CONFIG_OVERRIDE
 #define FC_FW_CFG 256, 256, 4, 2, 64, 2, 8 | 4096
-#define FC_DG_CFG 224, 256, 1, 8, 64, 2, 1 | 2
+#define FC_DG_CFG 224, 256, 1, 8, 64, 2, 1 | 2 | 128
 #define FC_WG_CFG 256, 224, 4, 2, 64, 2
 #include "../freeimpala_amd/csrc/fc_gemm.hip"
 
@@ -77,7 +77,12 @@ int main(int argc, char** argv) {
 #define WGV(nm, S, ...) add("wgrd " nm, 2, [&](hipStream_t st, int k) { return fc_wgrad_impl<__VA_ARGS__>(a3, dh, slab, dw[k], R, st, S); }, dw[0], dw[1], (size_t)FCK * FCO * 4)
     // the shipped configurations first (fc_gemm.hip FC_*_CFG), then alternatives
     FWDV("256x256 w4x2 bk64 ns2 ntY midbar", 256, 256, 4, 2, 64, 2, 8 | 4096);
+    DGV("224x256 w1x8 bk64 ns2 prio ntst xrow", 224, 256, 1, 8, 64, 2, 1 | 2 | 128);
     DGV("224x256 w1x8 bk64 ns2 prio ntst", 224, 256, 1, 8, 64, 2, 1 | 2);
+    DGV("224x256 w1x8 bk64 ns2 prio xrow", 224, 256, 1, 8, 64, 2, 1 | 128);
+    DGV("224x256 w1x8 bk64 ns2 prio", 224, 256, 1, 8, 64, 2, 1);
+    DGV("448x128 w4x2 bk64 ns2 prio xrow", 448, 128, 4, 2, 64, 2, 1 | 128);
+    DGV("448x128 w4x2 bk64 ns2 prio ntst xrow", 448, 128, 4, 2, 64, 2, 1 | 2 | 128);
     WGV("256x224 w4x2 bk64 ns2", 9, 256, 224, 4, 2, 64, 2);
     std::vector<std::vector<float>> ms(vs.size());
     hipEvent_t e0, e1;
