@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
-"""Timing-only copy of atari_fr.hip with per-phase clock sums in conv12_fwd_fr2 (waves 0 and 4),
+"""Timing-only copy of atari_fr.hip with per-phase clock sums in conv12_fwd_fr (waves 0 and 4),
 written to build/exp2/atari_fr.hip; build it with
-  SRC=build/exp2/atari_fr.hip bash scripts/build_exp.sh c12ph -DFI_C12_V2=1 [-DFI_C12_SPLIT=c,a,b]
-The launcher prints '[phases conv12_fwd_fr2 wave W] clk/frame: B1 phaseA phaseB B2' on the 4th call.
+  SRC=build/exp2/atari_fr.hip bash scripts/build_exp.sh c12ph 
+The launcher prints '[phases conv12_fwd_fr wave W] clk/frame: B1 phaseA phaseB B2' on the 4th call.
 Buckets: 1 = B1 wait, 2 = phase A, 3 = phase B, 4 = B2 wait."""
 import os, re
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -37,23 +37,23 @@ static void ph_report(const char* name, int grid) {
 }
 '''
 src = src.replace('namespace fi {\n', 'namespace fi {\n' + macros, 1)
-k0 = src.index('void conv12_fwd_fr2(')
-k1 = src.index('#ifndef FI_C12_V2')
+k0 = src.index('void conv12_fwd_fr(')
+k1 = src.index('int conv12_fwd_fr_launch(')
 ker = src[k0:k1]
 def sub(old, new, count):
     global ker
     assert ker.count(old) == count, (old, ker.count(old))
     ker = ker.replace(old, new)
 sub('        for (int it = 0; it <= nmine; ++it) {\n', '        PH_DECL\n        for (int it = 0; it <= nmine; ++it) {\n            PH(3);\n            PH_ITER();\n', 2)
-sub('            lds_barrier();  // B1: image(it) complete; conv2 image read by conv2(it-2)\n',
-    '            lds_barrier();  // B1: image(it) complete; conv2 image read by conv2(it-2)\n            PH(1);\n', 1)
+sub('            lds_barrier();  // B1: image(it) complete; the conv2 image read by conv2(it-2)\n',
+    '            lds_barrier();  // B1: image(it) complete; the conv2 image read by conv2(it-2)\n            PH(1);\n', 1)
 sub('            lds_barrier();  // B1\n', '            lds_barrier();  // B1\n            PH(1);\n', 1)
-sub('            lds_barrier();  // B2: conv2 image complete\n', '            PH(2);\n            lds_barrier();  // B2: conv2 image complete\n            PH(4);\n', 1)
+sub('            lds_barrier();  // B2: the conv2 image complete\n', '            PH(2);\n            lds_barrier();  // B2: the conv2 image complete\n            PH(4);\n', 1)
 sub('            lds_barrier();  // B2: a1(it-1) in the conv2 image\n', '            PH(2);\n            lds_barrier();  // B2: a1(it-1) in the conv2 image\n            PH(4);\n', 1)
 sub('        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");\n', '        PH(3);\n        PH_FLUSH();\n        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");\n', 2)
 src = src[:k0] + ker + src[k1:]
 src = src.replace('                       a1_planar);\n    FI_HIP_CHECK(hipGetLastError());\n    return FI_OK;\n}',
-                  '                       a1_planar);\n    FI_HIP_CHECK(hipGetLastError());\n    ph_report("conv12_fwd_fr2", grid);\n    return FI_OK;\n}', 1)
+                  '                       a1_planar);\n    FI_HIP_CHECK(hipGetLastError());\n    ph_report("conv12_fwd_fr", grid);\n    return FI_OK;\n}', 1)
 os.makedirs(os.path.join(ROOT, "build/exp2"), exist_ok=True)
 open(os.path.join(ROOT, "build/exp2/atari_fr.hip"), "w").write(src)
 print("wrote build/exp2/atari_fr.hip")
