@@ -302,13 +302,17 @@ def test_fused_conv21_backward_without_da1_store(monkeypatch):
     np.testing.assert_array_equal(gs[0], gs[1])
 
 
-@pytest.mark.parametrize("T,B", [(3, 4096), (11, 1365)])  # 16,384 frames; 16,380 (ragged tiles)
+# 16,384 frames; 16,380 (ragged tiles); 1,500 (the dgrad's 1,000 rows = 4 tile rows over 56
+# workgroups: its XCD row chunks leave four XCDs without rows)
+@pytest.mark.parametrize("T,B", [(3, 4096), (11, 1365), (2, 500)])
 def test_fc_layer_kernels_vs_fp32_gemm(orc, T, B, monkeypatch):
     """The hand-written fc kernels (fc_gemm.hip) at sizes where every persistent workgroup of
     the forward / dgrad walks several output tiles (the staging pipeline running across tile
     boundaries) and the weight gradient splits R into 9 slabs, against fp32 GEMMs of the GPU's
     own bf16 inputs: h = relu(a3 . W + b) and da3 = dh . W^T to a bf16 rounding, dW = a3^T . dh
-    to fp32 summation-order rounding. R = 16,380 leaves a partial last row tile."""
+    to fp32 summation-order rounding. R = 16,380 leaves a partial last row tile; the dgrad deals
+    its tile rows to XCDs in contiguous eighths (fc_nt_kernel OPT 128), including eighths with no
+    rows at the smallest size."""
     N = (T + 1) * B
     L = mk(T=T, B=B, seed=6)
     L.synth(seed=23)
