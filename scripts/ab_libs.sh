@@ -5,5 +5,5 @@ for L in "$@"; do
   [ "$L" = prod ] && L=""
   FI_LIB_OVERRIDE=$L timeout -k 10 200 python bench.py --steps 8 --warmup 3 --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/ab.json 2>gpurun_out/ab.err || exit 1
   python3 -c "
-import json; d=json.load(open('gpurun_out/ab.json')); k=d['kernel_ms_per_step']; print('${L:-prod}', round(d['ms_per_step'],3), {x: k[x] for x in list(k)[:7]})"
+import json, os; d=json.load(open('gpurun_out/ab.json')); k=d['kernel_ms_per_step']; sel=os.environ.get('AB_KERNELS'); print('${L:-prod}', round(d['ms_per_step'],3), {x: k[x] for x in (sel.split(',') if sel else list(k)[:7]) if x in k})"
 done
