@@ -498,16 +498,27 @@ __global__ __launch_bounds__(512) void fc_tn_kernel(const __bf16* __restrict__ X
     // follow (XCD-contiguous when there is no whole slice per XCD, i.e. small R)
     const int NT = ntx * nty, per = (int)(gridDim.x / NT) / 8;
     const int b = blockIdx.x, j = b / 8;
-    int sp, rem;
+    int sp, rem, tx, ty;
     if (j < per * NT) {
         sp = (b % 8) * per + j / NT;
         rem = j - (j / NT) * NT;
+        tx = rem / nty, ty = rem - tx * nty;
+    } else if (per > 0 && (int)gridDim.x == (8 * per + 1) * NT && ntx == 2 && nty == 14) {
+        // one leftover slice of 2 x 14 tiles (the fc weight gradient at 9 slices): block b runs on
+        // XCD x = b % 8 as its slot r = (b - 8 per NT) / 8. XCDs 0-3 take 2 x 2 tile blocks (ty 2x,
+        // 2x+1, both tx), XCDs 4-7 1 x 3 blocks (one tx, three of ty 8..13), so each XCD reads few
+        // of the slice's column blocks: 14.6 instead of 20 slice-units of HBM reads (dh column
+        // half = 0.5, a3 column block = 0.43; once = 7)
+        const int id = b - 8 * per * NT, x = id % 8, r = id / 8;
+        sp = 8 * per;
+        if (x < 4) tx = r & 1, ty = 2 * x + (r >> 1);
+        else tx = (x - 4) >> 1, ty = 8 + 3 * ((x - 4) & 1) + r;
     } else {
         const int id = per > 0 ? b - 8 * per * NT : xcd_remap(b, gridDim.x);
         sp = 8 * per + id / NT;
         rem = id - (id / NT) * NT;
+        tx = rem / nty, ty = rem - tx * nty;
     }
-    const int tx = rem / nty, ty = rem - tx * nty;
     const int x0 = tx * BX, y0 = ty * BY;
     const int rbeg = sp * rps, rend = min(R, rbeg + rps);
     const int nk = rend > rbeg ? (rend - rbeg + BK - 1) / BK : 0;

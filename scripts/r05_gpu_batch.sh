@@ -1,2 +1,3 @@
-# round-5 GPU batch (A/B experiments): conv3 forward on 32x32x16 MFMAs with two accumulator chains (read-ahead 4 / 8)
-AB_KERNELS=conv3_fwd,conv12_fwd ROUNDS=2 timeout -k 10 600 bash scripts/ab_rounds.sh prod build/ab/lib_wide2.so build/ab/lib_wide2p8.so > gpurun_out/ab_wide2.txt 2>&1
+# round-5 GPU batch (A/B experiments): fc weight gradient with the leftover slice's tiles dealt to XCDs in blocks (lib_wg)
+FI_LIB_OVERRIDE=$PWD/build/ab/lib_wg.so ARCH=atari TAG=wg bash scripts/pmc_pass.sh > gpurun_out/pmc_wg.txt 2>&1 || exit 1
+AB_KERNELS=fc_wgrad,fc_dgrad,fc_fwd ROUNDS=3 timeout -k 10 600 bash scripts/ab_rounds.sh prod build/ab/lib_wg.so > gpurun_out/ab_wg.txt 2>&1
