@@ -84,11 +84,16 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_base) {
         : "memory");
 }
 
-// Streaming 16-byte store of an output tile (nontemporal unless FI_PLAIN_STORES: A/B knob).
-#ifdef FI_PLAIN_STORES
-#define FI_ST16(v, p) (*(p) = (v))
-#else
+// 16-byte store of a frame-resident kernel's output (default cache policy; FI_NT_STORES: the
+// non-temporal policy, A/B knob). Round 5: with non-temporal stores the lines that two waves of a
+// workgroup fill in halves (a3, a2, da2: 64 B each) left the L2 as separate partial writes --
+// conv12_fwd 27.6, conv3_fwd 7.65, conv3_bwd 15.0 GB per launch; with the default policy they merge
+// in the L2: 26.6 / 6.89 / 13.7 GB (1.00x algorithmic), the step 0.07 ms shorter
+// (profiles/r05_plain_stores_ab.txt)
+#ifdef FI_NT_STORES
 #define FI_ST16(v, p) __builtin_nontemporal_store((v), (p))
+#else
+#define FI_ST16(v, p) (*(p) = (v))
 #endif
 
 // Opaque copy: the compiler must assume x changed here, so values derived from it are
