@@ -6,7 +6,11 @@ policy backward -> [RCCL all-reduce] -> optimizer) over one (T, B) batch of synt
 trajectories already resident in HBM. value = T * B_per_gpu * N * K / max-over-ranks(time).
 
   python bench.py [--gpus N --steps K --warmup W] [--arch atari|mlp]
-  N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+  N > 1 either form: `python bench.py --gpus N` starts the N ranks itself (a child
+  `python -m torch.distributed.run --nproc-per-node N bench.py ...`, launched before anything
+  touches the GPU; rank 0's line is relayed, the child's exit code returned), or
+  `python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...` directly.
+  --gpus N with fewer than N visible devices, or disagreeing with a launcher's WORLD_SIZE, exits 2.
 
 The roofline object is measured live: HIP events around every kernel launch of a few
 profiled steps (after the timed region) give each kernel's mean duration; ALGORITHMIC work
@@ -217,6 +221,31 @@ def main():
                          f"one whole step when {CPU_FULL_GB} GB of host memory are free)")
     args = ap.parse_args()
 
+    # --gpus N without a launcher: start the N ranks as a child launcher process before this
+    # process touches the GPU (device counting through torch does not initialise it)
+    import socket
+    import subprocess
+    from freeimpala_amd.launch import LaunchError, bench_launch_plan
+
+    def visible_devices():
+        import torch
+        return torch.cuda.device_count()
+
+    def free_port():
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            return sk.getsockname()[1]
+
+    try:
+        cmd = bench_launch_plan(args.gpus, os.environ, sys.argv[1:], os.path.abspath(__file__),
+                                sys.executable, visible_devices, free_port())
+    except LaunchError as e:
+        print(f"bench.py: {e}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if cmd is not None:
+        print(f"bench.py: starting {args.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+        sys.exit(subprocess.run(cmd).returncode)
+
     ws, rank, local = dist_env()
     N = max(ws, 1)
     # the learner library first: it then binds the image's ROCm 7.2 runtime and RCCL
@@ -233,8 +262,9 @@ def main():
         dist.init_process_group("gloo", rank=rank, world_size=ws)
 
     from freeimpala_amd.launch import (broadcast_bytes, data_parallel_fields, gather_objects, max_over_ranks,
-                                       shard_columns)
+                                       shard_columns, timed_steps)
     from freeimpala_amd.learner import DeviceLearner
+    from freeimpala_amd.roofline import step_roofline
 
     T, B, A = args.seq_len, args.batch, args.num_actions
     # rehearsal knobs for a one-GPU box (never set by the driver): FI_BENCH_DEVICE pins every
@@ -256,14 +286,8 @@ def main():
 
     for _ in range(args.warmup):
         L.step_resident(stats=False)
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        L.step_resident(stats=False)
-    L.sync()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    own_ms_per_step = 1000.0 * elapsed / args.steps  # this rank's own clock, before the max
+    own, elapsed = timed_steps(lambda: L.step_resident(stats=False), L.sync, barrier, args.steps)
+    own_ms_per_step = 1000.0 * own / args.steps  # this rank's own clock: drained, before the closing barrier
     if ws > 1:
         elapsed = max_over_ranks(elapsed)
     ms_per_step = 1000.0 * elapsed / args.steps
@@ -348,6 +372,18 @@ def main():
                                       "frac": round(work["vtrace"][1] / (vt_warm_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                                       "method": f"{VT_REPLAYS} launches on the same resident tensors (cache-warm)"},
                                 in_step_event_ms=round(kt["vtrace"]["ms"], 5) if "vtrace" in kt else None),
+        # the whole step against its floors: stamped PMC bytes / the timed ms_per_step, and every
+        # kernel's gap to max(HBM, MFMA) floor (freeimpala_amd/roofline.py)
+        "step_roofline": dict(step_roofline(per_step, {k: v["count"] / max(1, args.profile_steps) for k, v in kt.items()},
+                                            work, traffic, mfma, ms_per_step, dtype),
+                              counters_file=counters_build.get("traffic_file")),
+        # NOT a decomposition of ms_per_step: these come from the profiled pass after the timed loop
+        "breakdown_source": {
+            "fields": ["kernel_ms_per_step", "phase_ms", "step_roofline.kernels_by_gap"],
+            "pass": (f"{args.profile_steps} profiled steps after the timed loop, a HIP event pair around "
+                     "every launch (the events add a little time; the timed loop has none)"),
+            "profiled_ms_per_step": round(sum(v for k, v in phases.items() if k != "steps"), 4),
+            "timed_ms_per_step": round(ms_per_step, 4)},
         "kernel_ms_per_step": {k: round(v, 4) for k, v in sorted(per_step.items(), key=lambda x: -x[1])},
         "phase_ms": {k: round(v, 4) for k, v in phases.items() if k != "steps"},
         "final_loss": st["total_loss"], "grad_norm": st["grad_norm"],

@@ -8,6 +8,11 @@
 
 namespace fi {
 
+// partial conv1 weight-gradient slabs per workgroup of the fused conv2 backward + conv1 weight
+// gradient (blocked fp32 accumulation over the workgroup's frames, atari_fr.hip): the kernel
+// writes this many slabs per workgroup, atari.hip sizes the slab region and reduces that many
+constexpr int kC1Segs = 8;
+
 // per-launch timing hook (implemented by the learner's profiling events)
 struct KernelTagger {
     virtual void begin(const char* name) = 0;

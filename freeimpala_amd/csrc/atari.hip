@@ -765,10 +765,8 @@ static bool dmalloc(AtariImpl* I, T** p, size_t n) {
 
 // split factors (blocks over the reduction) per weight-gradient GEMM
 constexpr int SPL_H = 128, SPL_FC = 9, SPL_C3 = 160, SPL_C2 = 256, SPL_C1 = 512;
-// partial conv1 weight-gradient slabs per frame-resident workgroup of the fused conv2 backward +
-// conv1 weight gradient (atari_fr.hip SEGS: blocked fp32 accumulation over the workgroup's
-// frames): conv2 [grid][512][64], then conv1 [grid][kC1Segs][256][32]
-constexpr int kC1Segs = 8;
+// the fused conv2 backward + conv1 weight gradient's slabs: conv2 [grid][512][64], then conv1
+// [grid][kC1Segs][256][32] (kC1Segs: atari.h, shared with atari_fr.hip's writer)
 constexpr int GBM = 128;  // M-tile of the dgrad GEMMs (class stride granularity)
 
 AtariNet* atari_create(int B, int T, int A) {

@@ -70,7 +70,7 @@ constexpr int OUT = 400 * 32 * 2;                   // 25,600 B output / dY tile
 // (profiles/r05_blocked_accumulation_ab.txt): a second conv1 register set, conv2 slabs flushed
 // from inside the frame loop, and both roles walking a segment loop nest cost conv21 0.14, 0.17
 // and 0.5 ms.
-constexpr int SEGS = 8;
+constexpr int SEGS = kC1Segs;  // atari.h: the slab count atari.hip allocates and reduces
 __device__ __forceinline__ int seg_last(int k, int nmine) { return ((k + 1) * nmine) / SEGS - 1; }
 
 // one conv2 weight-gradient slab [512][64] from a wave's accumulators (kernel row wr), zeroing
@@ -1651,9 +1651,9 @@ __global__ __launch_bounds__(512, 2) void conv21_bwd_fr(const __bf16* __restrict
                 case 2: conv1_wgrad(std::integral_constant<int, 2>{}); break;
                 default: conv1_wgrad(std::integral_constant<int, 3>{}); break;
             }
-            // a segment ends here (at most one per frame once nmine >= SEGS; with fewer frames the
-            // leading segments are empty and everything lands in the slabs flushed after the
-            // loop). Marked unlikely: the block is placed out of the frame loop's code -- the
+            // a segment ends here (at most one per frame once nmine >= SEGS; with fewer frames than
+            // SEGS, seg_last(0) is -1, so every frame lands in segment 0 and the trailing segments
+            // are written as zero slabs after the loop). Marked unlikely: the block is placed out of the frame loop's code -- the
             // flush inlined in line cost conv21 0.45 ms though it runs 8 times per workgroup
             if (__builtin_expect(it == seg_last(sg, nmine), 0)) c1_flush();
         }

@@ -30,6 +30,7 @@
 #include "fi_common.h"
 #include "kernels.h"
 
+#include <atomic>
 #include <algorithm>
 #include <cmath>
 #include <mutex>
@@ -1023,12 +1024,24 @@ static int seq_grid(int B) {
 static bool lds_supported(int A, int B) { return B % 8 == 0 && A % 2 == 0 && A >= 2 && A <= 20; }
 
 template <int A>
-static void launch_str(const VtArgs& a, int nblk, hipStream_t s) {
-    // more than 64 KB of dynamic LDS: raise the kernel's limit on the calling thread's current
-    // device before every launch (cheap; a once-per-process flag would only cover the first device)
-    (void)hipFuncSetAttribute((const void*)vtrace_stream_kernel<A>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
+static int launch_str(const VtArgs& a, int nblk, hipStream_t s) {
+    // more than 64 KB of dynamic LDS: the kernel's limit is raised once per device (a bit per
+    // device id; handles on different devices launch from their own threads)
+    static std::atomic<uint64_t> raised{0};
+    int dev = 0;
+    FI_HIP_CHECK(hipGetDevice(&dev));
+    const uint64_t bit = dev < 64 ? (uint64_t)1 << dev : 0;
+    if (!bit || !(raised.load(std::memory_order_acquire) & bit)) {
+        const hipError_t e = hipFuncSetAttribute((const void*)vtrace_stream_kernel<A>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess)
+            return fail(FI_ERR_HIP, std::string("vtrace: the streaming kernel needs 160 KB of LDS per workgroup "
+                                                "(hipFuncSetAttribute MaxDynamicSharedMemorySize: ") +
+                                        hipGetErrorString(e) + ")");
+        raised.fetch_or(bit, std::memory_order_acq_rel);
+    }
     hipLaunchKernelGGL(vtrace_stream_kernel<A>, dim3(nblk), dim3(VtStr<A>::NT), VtStr<A>::lds_bytes(a.T), s, a);
+    return FI_OK;
 }
 // persistent grid of the streaming kernel: one workgroup per CU (132 KB of LDS at T = 100)
 static int str_grid(int B) {
@@ -1108,16 +1121,16 @@ int vtrace_launch(int variant, int T, int B, int A, const float* pi, const float
                    "vtrace: streaming kernel needs 16-byte aligned tensors");
         const int nblk = str_grid(B);
         switch (A) {
-            case 2: launch_str<2>(a, nblk, stream); break;
-            case 4: launch_str<4>(a, nblk, stream); break;
-            case 6: launch_str<6>(a, nblk, stream); break;
-            case 8: launch_str<8>(a, nblk, stream); break;
-            case 10: launch_str<10>(a, nblk, stream); break;
-            case 12: launch_str<12>(a, nblk, stream); break;
-            case 14: launch_str<14>(a, nblk, stream); break;
-            case 16: launch_str<16>(a, nblk, stream); break;
-            case 18: launch_str<18>(a, nblk, stream); break;
-            case 20: launch_str<20>(a, nblk, stream); break;
+            case 2: FI_TRY(launch_str<2>(a, nblk, stream)); break;
+            case 4: FI_TRY(launch_str<4>(a, nblk, stream)); break;
+            case 6: FI_TRY(launch_str<6>(a, nblk, stream)); break;
+            case 8: FI_TRY(launch_str<8>(a, nblk, stream)); break;
+            case 10: FI_TRY(launch_str<10>(a, nblk, stream)); break;
+            case 12: FI_TRY(launch_str<12>(a, nblk, stream)); break;
+            case 14: FI_TRY(launch_str<14>(a, nblk, stream)); break;
+            case 16: FI_TRY(launch_str<16>(a, nblk, stream)); break;
+            case 18: FI_TRY(launch_str<18>(a, nblk, stream)); break;
+            case 20: FI_TRY(launch_str<20>(a, nblk, stream)); break;
             default: return fail(FI_ERR_UNSUPPORTED, "vtrace: A not instantiated");
         }
         FI_HIP_CHECK(hipGetLastError());

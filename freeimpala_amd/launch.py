@@ -11,12 +11,66 @@ here so that it can be exercised on CPU with the gloo backend (tests/test_dist_g
                            N contiguous per-GPU shards (reference data_structures.h:267-300);
   * gather_objects / data_parallel_fields -- bench.py's N > 1 line: every rank's own ms/step,
                            its exposed all-reduce wait and the bytes all-reduced per step, so a
-                           scaling run explains itself (weak-scaling loss vs exposed exchange).
+                           scaling run explains itself (weak-scaling loss vs exposed exchange);
+  * bench_launch_plan   -- `python bench.py --gpus N` without a launcher: the torch.distributed.run
+                           command that starts the N ranks (decided before anything touches the GPU);
+  * timed_steps         -- the timed loop: a rank's own time and the barrier-bracketed time.
 torch.distributed is plumbing only; the product math never goes through it.
 """
 from __future__ import annotations
 
-from typing import Sequence
+import time
+from typing import Callable, Mapping, Sequence
+
+# environment a torch.distributed launcher sets in every rank it starts
+LAUNCHER_ENV = ("WORLD_SIZE", "LOCAL_RANK", "TORCHELASTIC_RUN_ID")
+
+
+class LaunchError(RuntimeError):
+    """bench.py was asked for a GPU count it cannot honour."""
+
+
+def bench_launch_plan(gpus: int, env: Mapping[str, str], argv: Sequence[str], script: str,
+                      python: str, visible_devices: Callable[[], int], port: int) -> list | None:
+    """How bench.py runs for `--gpus N` (BASELINE metric: 1/2/4/8 MI355X, one process per GPU).
+
+    Returns None when this process is one of the ranks already (N == 1, or started by a
+    launcher whose WORLD_SIZE equals N), else the command of the child launcher that starts N
+    ranks of the same script with the same arguments; the caller runs it as a child process and
+    exits with its code (never an exec: the parent has not touched the GPU, and must not).
+    Raises LaunchError when --gpus disagrees with the launcher's WORLD_SIZE, or when fewer than N
+    devices are visible (FI_BENCH_DEVICE, the one-device rehearsal that pins every rank to one
+    device, needs one). `visible_devices` is only called when ranks must be started."""
+    if gpus < 1:
+        raise LaunchError(f"--gpus must be >= 1 (got {gpus})")
+    if any(k in env for k in LAUNCHER_ENV):
+        ws = int(env.get("WORLD_SIZE", "1"))
+        if ws != gpus:
+            raise LaunchError(f"--gpus {gpus} disagrees with the launcher's WORLD_SIZE={ws}")
+        return None
+    if gpus == 1:
+        return None
+    need = 1 if env.get("FI_BENCH_DEVICE") not in (None, "") else gpus
+    have = int(visible_devices())
+    if have < need:
+        raise LaunchError(f"--gpus {gpus} needs {need} visible GPU(s), {have} visible")
+    return [python, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", script, *argv]
+
+
+def timed_steps(step: Callable[[], object], sync: Callable[[], object], barrier: Callable[[], object],
+                steps: int) -> tuple[float, float]:
+    """(own, bracketed) seconds for `steps` steps. Both start after a barrier; `own` stops when
+    this rank's device work has drained (before the closing barrier, so it is this rank's time
+    alone); `bracketed` stops after the closing barrier (what the max over ranks is taken of)."""
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    own = time.perf_counter() - t0
+    barrier()
+    return own, time.perf_counter() - t0
 
 
 def shard_columns(rank: int, world: int, b_per_rank: int) -> tuple[int, int]:
@@ -68,7 +122,8 @@ def gather_objects(obj) -> list:
 def data_parallel_fields(per_rank: Sequence[dict], grad_bytes: int, buckets: int | None) -> dict:
     """The N > 1 fields of bench.py's line from every rank's own measurements.
 
-    per_rank[r] = {"ms_per_step": the rank's own timed-loop ms/step (before the max over ranks),
+    per_rank[r] = {"ms_per_step": the rank's own timed-loop ms/step (its device work drained,
+                                  before the closing barrier and the max over ranks),
                    "allreduce_ms": the rank's exposed all-reduce wait per step (the learner's
                    "allreduce" phase: the compute stream waiting for buckets still in flight
                    after the backward, HIP events over the profiled steps)}.
