@@ -121,3 +121,26 @@ def test_timed_steps_order():
     log = []
     own, br = timed_steps(lambda: log.append("s"), lambda: log.append("sync"), lambda: log.append("b"), 3)
     assert log == ["b", "s", "s", "s", "sync", "b"] and 0 <= own <= br
+
+
+@pytest.mark.gpu
+def test_bench_gpus2_spawns_two_ranks_on_the_gpu_box():
+    """The driver's command form at N = 2 on a one-GPU box: `python bench.py --gpus 2` starts
+    two ranks itself; FI_BENCH_DEVICE=0 pins both to the one device and FI_BENCH_NO_COMM skips
+    the RCCL communicator (RCCL refuses two ranks on one device). One JSON line, n_gpus 2, the
+    per-rank data_parallel fields."""
+    import json
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "LOCAL_RANK", "RANK",
+                                                               "TORCHELASTIC_RUN_ID")}
+    env.update(FI_BENCH_DEVICE="0", FI_BENCH_NO_COMM="1")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--arch", "mlp",
+                        "--steps", "3", "--warmup", "1", "--profile-steps", "1", "--no-cpu-baseline"],
+                       env=env, capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 2 * d["config"]["B_per_gpu"]
+    dp = d["data_parallel"]
+    assert dp["ranks"] == 2 and len(dp["rank_ms_per_step"]["per_rank"]) == 2
+    assert "step_roofline" in d and d["breakdown_source"]["timed_ms_per_step"] == d["ms_per_step"]
