@@ -36,6 +36,7 @@ TAGS = {
         "fc_dgrad": ("fcg::EpiDgrad", 1, 0),
         "heads_dgrad": ("heads_dgrad", 1, 0),
         "heads_wgrad": ("heads_wgrad", 1, 0),
+        "heads_fwd": ("EpiHeads", 1, 0),
     },
     "mlp": {
         "vtrace": ("vtrace_lds_kernel", 1, 0),
