@@ -212,6 +212,8 @@ def main():
     ap.add_argument("--batch", type=int, default=4096, help="per-GPU batch (weak scaling)")
     ap.add_argument("--num-actions", type=int, default=18)
     ap.add_argument("--profile-steps", type=int, default=3)
+    ap.add_argument("--sustain-seconds", type=float, default=10.0,
+                    help="after the timed loop, run the step this long more and report the sustained rate")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-full", action="store_true",
@@ -293,6 +295,20 @@ def main():
     ms_per_step = 1000.0 * elapsed / args.steps
     value = T * B * N * args.steps / elapsed
 
+    # ---- sustained rate: the same step for --sustain-seconds more (untimed for `value`): the
+    # power-limited clock's steady state beside the K-step burst, and GPU activity long enough
+    # for a coarse utilisation sampler to see. Every rank runs the same step count (from the
+    # max-over-ranks time), so the in-step all-reduces pair up.
+    sustained = None
+    if args.sustain_seconds > 0:
+        n_sus = max(1, int(args.sustain_seconds * 1000.0 / ms_per_step))
+        s_own, s_el = timed_steps(lambda: L.step_resident(stats=False), L.sync, barrier, n_sus)
+        if ws > 1:
+            s_el = max_over_ranks(s_el)
+        sustained = {"steps": n_sus, "ms_per_step": round(1000.0 * s_el / n_sus, 4),
+                     "value": round(T * B * N * n_sus / s_el, 1),
+                     "note": "the same step after the timed loop, run for ~--sustain-seconds; not `value`"}
+
     # ---- live per-kernel timing (HIP events on the learner stream) for the roofline
     L.set_profiling(True)
     for _ in range(args.profile_steps):
@@ -361,6 +377,7 @@ def main():
             "T": T, "B_per_gpu": B, "A": A, "global_batch": B * N, "seq_len": T,
             "parallelism": f"dp{N}", "optimizer": "adam", "policy": args.arch,
         },
+        "sustained": sustained,
         "roofline": roof(dominant) if dominant else None,
         # V-trace scan: ~20 us, so per-launch event brackets inside the step carry the dispatch
         # latency; the burst of VT_REPLAYS back-to-back launches on the same resident tensors is the

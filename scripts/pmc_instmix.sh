@@ -23,7 +23,7 @@ for SET in "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM
   i=$((i + 1))
   rm -rf "$OUT/pmcmix_$i"
   timeout -s KILL 90 rocprofv3 --pmc $SET --output-format csv -d "$OUT/pmcmix_$i" -o run \
-      -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --profile-steps 1 --no-cpu-baseline \
+      -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --profile-steps 1 --sustain-seconds 0 --no-cpu-baseline \
       > "$OUT/pmcmix_$i.log" 2>&1
   rc=$?
   echo "pass $i rc=$rc: $SET"

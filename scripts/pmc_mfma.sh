@@ -14,7 +14,7 @@ export TMPDIR=/tmp
 cd /tmp
 rm -rf "$OUT/pmc_mfma_${ARCH}_$TAG"
 timeout -s KILL 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv \
-    -d "$OUT/pmc_mfma_${ARCH}_$TAG" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --profile-steps 1 \
+    -d "$OUT/pmc_mfma_${ARCH}_$TAG" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --profile-steps 1 --sustain-seconds 0 \
     --no-cpu-baseline > "$OUT/pmc_mfma_${ARCH}_$TAG.log" 2>&1
 rc=$?
 [ $rc -ne 0 ] && { echo "pmc rc=$rc"; tail -5 "$OUT/pmc_mfma_${ARCH}_$TAG.log"; exit $rc; }

@@ -13,7 +13,7 @@ cd /tmp
 for C in FETCH_SIZE WRITE_SIZE; do
   rm -rf "$OUT/pmc_${C}_${ARCH}_$TAG"
   timeout -s KILL 300 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_${C}_${ARCH}_$TAG" -o run \
-      -- python3 "$ROOT/bench.py" --arch "$ARCH" --steps 2 --warmup 1 --profile-steps 1 --no-cpu-baseline \
+      -- python3 "$ROOT/bench.py" --arch "$ARCH" --steps 2 --warmup 1 --profile-steps 1 --sustain-seconds 0 --no-cpu-baseline \
       > "$OUT/pmc_${C}_${ARCH}_$TAG.log" 2>&1
   rc=$?; echo "pmc $C rc=$rc"
   [ $rc -ne 0 ] && exit $rc

@@ -27,7 +27,7 @@ cd /tmp
 for A in atari mlp; do
   rm -rf "$OUT/prof_${A}_$TAG"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_${A}_$TAG" -o run \
-      -- python3 "$ROOT/bench.py" --arch $A --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/prof_${A}_$TAG.log" 2>&1
+      -- python3 "$ROOT/bench.py" --arch $A --steps 5 --warmup 2 --sustain-seconds 0 --no-cpu-baseline > "$OUT/prof_${A}_$TAG.log" 2>&1
   rc=$?; echo "rocprof $A rc=$rc"; [ $rc -ne 0 ] && exit $rc
 done
 exit 0

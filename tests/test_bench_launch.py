@@ -134,7 +134,8 @@ def test_bench_gpus2_spawns_two_ranks_on_the_gpu_box():
                                                                "TORCHELASTIC_RUN_ID")}
     env.update(FI_BENCH_DEVICE="0", FI_BENCH_NO_COMM="1")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--arch", "mlp",
-                        "--steps", "3", "--warmup", "1", "--profile-steps", "1", "--no-cpu-baseline"],
+                        "--steps", "3", "--warmup", "1", "--profile-steps", "1", "--sustain-seconds", "0.5",
+                        "--no-cpu-baseline"],
                        env=env, capture_output=True, text=True, timeout=240, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -144,3 +145,4 @@ def test_bench_gpus2_spawns_two_ranks_on_the_gpu_box():
     dp = d["data_parallel"]
     assert dp["ranks"] == 2 and len(dp["rank_ms_per_step"]["per_rank"]) == 2
     assert "step_roofline" in d and d["breakdown_source"]["timed_ms_per_step"] == d["ms_per_step"]
+    assert d["sustained"]["steps"] >= 1 and d["sustained"]["ms_per_step"] > 0
