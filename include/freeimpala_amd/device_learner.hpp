@@ -120,8 +120,14 @@ struct LearnerConfig {
     // library of the reference binaries): the reference's own -p/--players, -M/--batch-size and
     // -S/--entry-size (registered by its setupArgumentParser, cmd/freeimpala/main.cpp:45-72)
     // plus the flags add_learner_arguments() registers. Throws std::invalid_argument.
+    // (two overloads, not a defaulted `LearnerConfig()` argument: clang rejects a default
+    // argument that needs the class's member initializers inside the class definition)
     template <class Parser>
-    static LearnerConfig from_parser(const Parser& program, LearnerConfig c = LearnerConfig()) {
+    static LearnerConfig from_parser(const Parser& program) {
+        return from_parser(program, LearnerConfig());
+    }
+    template <class Parser>
+    static LearnerConfig from_parser(const Parser& program, LearnerConfig c) {
         auto num = [](const std::string& f, const std::string& v) -> double {
             char* end = nullptr;
             const double x = std::strtod(v.c_str(), &end);

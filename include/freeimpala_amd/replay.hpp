@@ -258,7 +258,7 @@ class ModelManager {
 public:
     ModelManager(size_t num_players, size_t model_size, const std::string& directory)
         : models_(num_players), mu_(num_players), updated_(num_players), latest_(num_players),
-          dir_(directory), ckpt_counter_(num_players, 0) {
+          dir_(directory), ckpt_counter_(num_players) {
         for (size_t p = 0; p < num_players; ++p) {
             models_[p] = std::make_shared<Model>(model_size, latest_path(dir_, p));
             latest_[p].store(models_[p]->getVersion());
@@ -317,13 +317,18 @@ public:
     // Checkpoint: <dir>/model_<p>_<iter>.bin (iter 0: the next internal counter) and
     // <dir>/model_<p>_latest.bin, both `u64 version || blob`. Returns the versioned path
     // ("" on failure).
+    // Thread-safe where the reference is not (data_structures.h:395,402 read models[p] and the
+    // checkpoint counter unlocked): the model is read under the player's lock (getModel) and the
+    // counter is atomic, so checkpoint threads may save while the worker publishes
+    // (tests/cpp/race_check.cpp under ThreadSanitizer).
     std::string saveModel(size_t player_index, uint64_t current_iteration = 0) {
-        if (player_index >= models_.size() || !models_[player_index]) {
+        const auto cur = getModel(player_index);
+        if (!cur) {
             log_line("error", "Invalid model index or null model: " + std::to_string(player_index));
             return "";
         }
-        const auto snap = getModel(player_index)->createCopy();
-        const uint64_t it = current_iteration > 0 ? current_iteration : ckpt_counter_[player_index]++;
+        const auto snap = cur->createCopy();
+        const uint64_t it = current_iteration > 0 ? current_iteration : ckpt_counter_[player_index].fetch_add(1);
         const std::string vpath = iter_path(dir_, player_index, it);
         const std::vector<char> blob = snap->getData();
         if (!Model::fromData(vpath, blob, snap->getVersion())->saveToDisk()) {
@@ -376,7 +381,7 @@ private:
     std::vector<std::condition_variable> updated_;
     std::vector<std::atomic<uint64_t>> latest_;
     std::string dir_;
-    std::vector<uint64_t> ckpt_counter_;
+    std::vector<std::atomic<uint64_t>> ckpt_counter_;
 };
 
 }  // namespace freeimpala_amd

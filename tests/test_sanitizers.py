@@ -1,0 +1,51 @@
+"""Host code under sanitizers (the reference has none, and latent races).
+
+tests/cpp/race_check.cpp stresses the host side around the learner step from many threads:
+SharedBuffer writers / try_writers against readBatch / readBatchInto readers and draining,
+ModelManager publication against model copies, version polls, waits and concurrent checkpoint
+saves, MetricsTracker counters, and the SimLearner worker / checkpoint threads with actor
+threads (config #1's machinery). It is built twice and must finish clean both times:
+  * ThreadSanitizer (clang++ from /opt/rocm/lib/llvm: gcc 11's TSAN does not intercept
+    pthread_cond_clockwait, which libstdc++'s wait_for uses, and reports false double locks);
+  * AddressSanitizer + UndefinedBehaviorSanitizer (g++), every finding fatal.
+The TSAN build found a real race on its first run: ModelManager::saveModel read models_[p]
+(and the checkpoint counter) unlocked while updateModel wrote it -- the reference's own latent
+race (data_structures.h:395,402) carried into the restatement; saveModel now reads through the
+locked getModel and the counter is atomic. CPU only, no GPU and no libfi_learner.so.
+"""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "tests", "cpp", "race_check.cpp")
+CLANG = "/opt/rocm/lib/llvm/bin/clang++"
+
+
+def _build_and_run(tmp_path, compiler, flags, env_extra):
+    exe = str(tmp_path / "race_check")
+    cmd = [compiler, "-std=c++17", "-O1", "-g", *flags, "-I" + os.path.join(ROOT, "include"), SRC,
+           "-o", exe, "-pthread"]
+    b = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert b.returncode == 0, b.stderr[-4000:]
+    env = dict(os.environ, **env_extra)
+    r = subprocess.run([exe, str(tmp_path / "work")], capture_output=True, text=True, timeout=600, env=env)
+    return r
+
+
+@pytest.mark.skipif(not os.path.exists(CLANG), reason="no clang++ with the TSAN runtime")
+def test_host_side_is_race_free_under_tsan(tmp_path):
+    r = _build_and_run(tmp_path, CLANG, ["-fsanitize=thread"], {"TSAN_OPTIONS": "halt_on_error=1 exitcode=66"})
+    assert "WARNING: ThreadSanitizer" not in r.stderr, r.stderr[-6000:]
+    assert r.returncode == 0 and "OK race" in r.stdout, (r.returncode, r.stderr[-3000:])
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no g++")
+def test_host_side_clean_under_asan_ubsan(tmp_path):
+    r = _build_and_run(tmp_path, "g++", ["-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+                                         "-fno-omit-frame-pointer"],
+                       {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=0", "UBSAN_OPTIONS": "print_stacktrace=1"})
+    assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-6000:]
+    assert r.returncode == 0 and "OK race" in r.stdout, (r.returncode, r.stderr[-3000:])
