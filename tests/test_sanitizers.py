@@ -49,3 +49,24 @@ def test_host_side_clean_under_asan_ubsan(tmp_path):
                        {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=0", "UBSAN_OPTIONS": "print_stacktrace=1"})
     assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-6000:]
     assert r.returncode == 0 and "OK race" in r.stdout, (r.returncode, r.stderr[-3000:])
+
+
+MPIEXEC = shutil.which("mpiexec", path="/opt/conda/bin")
+
+
+@pytest.mark.skipif(not os.path.exists(CLANG) or MPIEXEC is None, reason="needs ROCm's clang++ and MPICH")
+def test_mpi_endpoint_is_race_free_under_tsan(tmp_path):
+    """The rank-0 MPI endpoint (include/freeimpala_amd/mpi_pool.hpp: receiver thread, processor
+    pool, per-player buffers, version / weights replies) against 4 actor ranks, every rank built
+    with ThreadSanitizer (tests/cpp/mpi_pool_check.cpp, the protocol test of tests/test_mpi.py)."""
+    exe = str(tmp_path / "mpi_pool_tsan")
+    b = subprocess.run([CLANG, "-std=c++17", "-O1", "-g", "-fsanitize=thread", "-I" + os.path.join(ROOT, "include"),
+                        "-I/opt/conda/include", os.path.join(ROOT, "tests", "cpp", "mpi_pool_check.cpp"), "-o", exe,
+                        "-pthread", "/opt/conda/lib/libmpi.so", "-Wl,--disable-new-dtags",
+                        "-Wl,-rpath,/usr/lib/x86_64-linux-gnu:/opt/conda/lib"], capture_output=True, text=True, timeout=600)
+    assert b.returncode == 0, b.stderr[-4000:]
+    env = dict(os.environ, HYDRA_LAUNCHER="fork", TSAN_OPTIONS="halt_on_error=1 exitcode=66")
+    r = subprocess.run([MPIEXEC, "-n", "5", exe, str(tmp_path / "work")], capture_output=True, text=True,
+                       timeout=300, env=env)
+    assert "WARNING: ThreadSanitizer" not in r.stdout + r.stderr, (r.stdout + r.stderr)[-6000:]
+    assert r.returncode == 0 and "OK mpi_pool actors=4" in r.stdout, (r.stdout + r.stderr)[-3000:]
