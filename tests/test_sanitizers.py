@@ -20,13 +20,18 @@ import subprocess
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SRC = os.path.join(ROOT, "tests", "cpp", "race_check.cpp")
 CLANG = "/opt/rocm/lib/llvm/bin/clang++"
 
 
-def _build_and_run(tmp_path, compiler, flags, env_extra):
-    exe = str(tmp_path / "race_check")
-    cmd = [compiler, "-std=c++17", "-O1", "-g", *flags, "-I" + os.path.join(ROOT, "include"), SRC,
+# (program, the line it prints when every check holds): the stress above, and the semantic
+# checks of the buffer / model store / flag parser (tests/cpp/replay_check.cpp)
+PROGRAMS = [("race_check", "OK race"), ("replay_check", "OK replay")]
+
+
+def _build_and_run(tmp_path, compiler, flags, env_extra, prog="race_check"):
+    exe = str(tmp_path / prog)
+    src = os.path.join(ROOT, "tests", "cpp", prog + ".cpp")
+    cmd = [compiler, "-std=c++17", "-O1", "-g", *flags, "-I" + os.path.join(ROOT, "include"), src,
            "-o", exe, "-pthread"]
     b = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
     assert b.returncode == 0, b.stderr[-4000:]
@@ -36,19 +41,21 @@ def _build_and_run(tmp_path, compiler, flags, env_extra):
 
 
 @pytest.mark.skipif(not os.path.exists(CLANG), reason="no clang++ with the TSAN runtime")
-def test_host_side_is_race_free_under_tsan(tmp_path):
-    r = _build_and_run(tmp_path, CLANG, ["-fsanitize=thread"], {"TSAN_OPTIONS": "halt_on_error=1 exitcode=66"})
+@pytest.mark.parametrize("prog,ok", PROGRAMS)
+def test_host_side_is_race_free_under_tsan(tmp_path, prog, ok):
+    r = _build_and_run(tmp_path, CLANG, ["-fsanitize=thread"], {"TSAN_OPTIONS": "halt_on_error=1 exitcode=66"}, prog)
     assert "WARNING: ThreadSanitizer" not in r.stderr, r.stderr[-6000:]
-    assert r.returncode == 0 and "OK race" in r.stdout, (r.returncode, r.stderr[-3000:])
+    assert r.returncode == 0 and ok in r.stdout, (r.returncode, r.stderr[-3000:])
 
 
 @pytest.mark.skipif(shutil.which("g++") is None, reason="no g++")
-def test_host_side_clean_under_asan_ubsan(tmp_path):
+@pytest.mark.parametrize("prog,ok", PROGRAMS)
+def test_host_side_clean_under_asan_ubsan(tmp_path, prog, ok):
     r = _build_and_run(tmp_path, "g++", ["-fsanitize=address,undefined", "-fno-sanitize-recover=all",
                                          "-fno-omit-frame-pointer"],
-                       {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=0", "UBSAN_OPTIONS": "print_stacktrace=1"})
+                       {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=0", "UBSAN_OPTIONS": "print_stacktrace=1"}, prog)
     assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-6000:]
-    assert r.returncode == 0 and "OK race" in r.stdout, (r.returncode, r.stderr[-3000:])
+    assert r.returncode == 0 and ok in r.stdout, (r.returncode, r.stderr[-3000:])
 
 
 MPIEXEC = shutil.which("mpiexec", path="/opt/conda/bin")
