@@ -77,3 +77,29 @@ def test_mpi_endpoint_is_race_free_under_tsan(tmp_path):
                        timeout=300, env=env)
     assert "WARNING: ThreadSanitizer" not in r.stdout + r.stderr, (r.stdout + r.stderr)[-6000:]
     assert r.returncode == 0 and "OK mpi_pool actors=4" in r.stdout, (r.stdout + r.stderr)[-3000:]
+
+
+@pytest.mark.skipif(not os.path.exists(CLANG), reason="no clang++ with the TSAN runtime")
+def test_cli_with_sim_learner_is_race_free_under_tsan(tmp_path):
+    """build/fi_freeimpala's whole threaded run (tools/fi_freeimpala.cpp: argument parsing, the
+    SimLearner's worker and checkpoint threads, 4 actor threads writing entries and syncing the
+    model, cleanup and the metrics line) built with ThreadSanitizer; `--learner sim` touches no
+    device, so libfi_learner.so is linked but never called."""
+    lib = os.path.join(ROOT, "freeimpala_amd", "lib")
+    if not os.path.exists(os.path.join(lib, "libfi_learner.so")):
+        pytest.skip("libfi_learner.so not built")
+    exe = str(tmp_path / "fi_freeimpala_tsan")
+    b = subprocess.run([CLANG, "-std=c++17", "-O1", "-g", "-fsanitize=thread", "-I" + os.path.join(ROOT, "include"),
+                        os.path.join(ROOT, "tools", "fi_freeimpala.cpp"), "-o", exe, "-pthread", "-L" + lib,
+                        "-lfi_learner", "-Wl,-rpath," + lib, "-Wl,-rpath,/opt/rocm/lib"],
+                       capture_output=True, text=True, timeout=600)
+    assert b.returncode == 0, b.stderr[-4000:]
+    r = subprocess.run([exe, "--learner", "sim", "--players", "2", "--iterations", "16", "--buffer-capacity", "8",
+                        "--batch-size", "4", "--agents", "4", "--learner-time", "0", "--agent-time", "0",
+                        "--entry-size", "8", "--game-steps", "8", "--seq-length", "3", "--checkpoint-freq", "2",
+                        "--checkpoint-location", str(tmp_path / "ck")],
+                       capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, TSAN_OPTIONS="halt_on_error=1 exitcode=66"))
+    assert "WARNING: ThreadSanitizer" not in r.stderr, r.stderr[-6000:]
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert '"learner_iterations": [16, 16]' in r.stdout
