@@ -103,3 +103,34 @@ def test_cli_with_sim_learner_is_race_free_under_tsan(tmp_path):
     assert "WARNING: ThreadSanitizer" not in r.stderr, r.stderr[-6000:]
     assert r.returncode == 0, r.stderr[-3000:]
     assert '"learner_iterations": [16, 16]' in r.stdout
+
+
+TSAN_BIN = os.path.join(ROOT, "build", "tsan")
+SUPP = os.path.join(ROOT, "tests", "tsan_rocm.supp")
+
+
+def _tsan_env():
+    return dict(os.environ, TSAN_OPTIONS=f"halt_on_error=0 exitcode=66 suppressions={SUPP}")
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(os.path.join(TSAN_BIN, "host_learner_check")),
+                    reason="build/tsan not built (make -f tests/cpp/tsan.mk)")
+def test_device_host_paths_race_free_under_tsan(tmp_path):
+    """The host side of the DEVICE learner under ThreadSanitizer on the GPU (the ROCm runtime,
+    uninstrumented, is suppressed: its own thread synchronisation is invisible to TSAN):
+      * tests/cpp/host_learner_check.cpp gpu -- two players stepping concurrently through the
+        C ABI from their own threads (DeviceLearner, pinned staging, async H2D);
+      * build/fi_freeimpala with the device learner -- 2 players, 4 actor threads, the
+        BasicLearner worker and checkpoint threads, model sync, stop()."""
+    r = subprocess.run([os.path.join(TSAN_BIN, "host_learner_check"), "gpu", str(tmp_path / "hlc")],
+                       capture_output=True, text=True, timeout=300, env=_tsan_env())
+    assert "WARNING: ThreadSanitizer" not in r.stderr, r.stderr[-6000:]
+    assert r.returncode == 0 and "OK gpu" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-3000:])
+    r = subprocess.run([os.path.join(TSAN_BIN, "fi_freeimpala"), "--players", "2", "--iterations", "32",
+                        "--buffer-capacity", "32", "--batch-size", "16", "--seq-length", "20", "--agents", "4",
+                        "--entry-size", "42", "--game-steps", "42", "--agent-time", "0", "--checkpoint-freq", "2",
+                        "--checkpoint-location", str(tmp_path / "ck")],
+                       capture_output=True, text=True, timeout=300, env=_tsan_env())
+    assert "WARNING: ThreadSanitizer" not in r.stderr, r.stderr[-6000:]
+    assert r.returncode == 0 and '"learner_iterations": [8, 8]' in r.stdout, (r.returncode, r.stderr[-3000:])
