@@ -172,27 +172,6 @@ struct ClassRows {
     }
 };
 
-// the heads' upstream gradient [rows][32]: dlogits (fp32, TB rows) | dvalue | 0 -> bf16
-struct DoutRows {
-    const float* dlog;
-    const float* dval;
-    int rows, TB, A;
-    __device__ void set_tile(int) {}
-    __device__ u32x4 load(int m, int kc) const {
-        if (m >= rows) return zero4();
-        bf16x8 o;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int c = kc * 8 + j;
-            float v = 0.f;
-            if (c < A) v = m < TB ? dlog[(size_t)m * A + c] : 0.f;
-            else if (c == A) v = dval[m];
-            o[j] = (__bf16)v;
-        }
-        return __builtin_bit_cast(u32x4, o);
-    }
-};
-
 // ------------------------------------------------------------------ epilogues
 struct EpiAct {  // out[m][n] = bf16(relu(acc*scale + bias[n]))
     __bf16* out;
@@ -214,15 +193,6 @@ struct EpiHeadsOut {
         v += bias[n];
         if (n < A) logits[(size_t)m * A + n] = v;
         else values[m] = v;
-    }
-};
-struct EpiMaskBf16 {  // out[m][n] = bf16(acc) if act[m][n] > 0 else 0
-    __bf16* out;
-    const __bf16* act;
-    int ld;
-    __device__ void operator()(int m, int n, float v) const {
-        const size_t i = (size_t)m * ld + n;
-        out[i] = (float)act[i] > 0.f ? (__bf16)v : (__bf16)0.f;
     }
 };
 template <int IH, int S>
@@ -466,43 +436,6 @@ static int wgrad(LA la, LB lb, float* slab, float* cs_slab, int M, int I, int J,
     return FI_OK;
 }
 
-// ------------------------------------------------------------------ small bf16 helpers
-// column sums of a row-major bf16 [M][C] tensor (C % 8 == 0, C <= 2048) into fp32 slabs
-// [kColsumSplits][C] (reduced in a fixed order by reduce_slabs: deterministic)
-constexpr int kColsumSplits = 512;
-__global__ __launch_bounds__(256) void colsum_bf16_kernel(const __bf16* __restrict__ Y, int M, int C,
-                                                         float* __restrict__ slab) {
-    __shared__ float red[2048];
-    const int tpr = C / 8;                     // threads per row
-    const int rpi = 256 / tpr;                 // rows per iteration
-    const int lr = threadIdx.x / tpr, c8 = threadIdx.x % tpr;
-    const int rows_per = (M + gridDim.x - 1) / gridDim.x;
-    const int r0 = blockIdx.x * rows_per, r1 = min(M, r0 + rows_per);
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (lr < rpi)
-        for (int r = r0 + lr; r < r1; r += rpi) {
-            const bf16x8 v = *(const bf16x8*)(Y + (size_t)r * C + 8 * c8);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) acc[j] += (float)v[j];
-        }
-    for (int i = threadIdx.x; i < C; i += 256) red[i] = 0.f;
-    __syncthreads();
-    for (int g = 0; g < rpi; ++g) {  // fixed order over the row groups
-        if (lr == g)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) red[8 * c8 + j] += acc[j];
-        __syncthreads();
-    }
-    for (int i = threadIdx.x; i < C; i += 256) slab[(size_t)blockIdx.x * C + i] = red[i];
-}
-
-static int colsum_bf16(const __bf16* Y, int M, int C, float* slab, hipStream_t s) {
-    FI_REQUIRE(C % 8 == 0 && C / 8 <= 256 && C <= 2048, "colsum_bf16: bad width");
-    hipLaunchKernelGGL(colsum_bf16_kernel, dim3(kColsumSplits), dim3(256), 0, s, Y, M, C, slab);
-    FI_HIP_CHECK(hipGetLastError());
-    return FI_OK;
-}
-
 // y *= (m > 0) elementwise (generic path only; the frame-resident conv3 backward masks in LDS)
 __global__ void relu_mask_bf16_kernel(__bf16* __restrict__ y, const __bf16* __restrict__ m, size_t n8) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n8; i += (size_t)gridDim.x * blockDim.x) {
@@ -522,7 +455,7 @@ static int relu_mask_bf16(__bf16* y, const __bf16* m, size_t n, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------ heads backward (VALU)
-// The heads are a 512 x (A+1) layer: K = A+1 = 19 is far too thin for MFMA tiles, so both
+// The heads are a 512 x (A+1) layer: K = A+1 <= 19 is far too thin for MFMA tiles, so both
 // backward products run on packed fp32 VALU with the weights / accumulators in registers.
 // A wave owns one row at a time (the row's upstream gradient dout[A+1] is wave-uniform:
 // scalar loads), each lane 8 consecutive hidden units.
@@ -649,19 +582,41 @@ __global__ __launch_bounds__(256, 1) void heads_wgrad_valu(const float* __restri
 }
 
 constexpr int kHeadsGrid = 512;
+constexpr int kHeadsDgradGrid = 1024;
 
-static int heads_wgrad_launch(const float* dlog, const float* dval, const __bf16* h, float* slab, float* cs, int R,
-                              int TB, hipStream_t s) {
-    hipLaunchKernelGGL(heads_wgrad_valu<19>, dim3(kHeadsGrid), dim3(256), 0, s, dlog, dval, h, slab, cs, R, TB);
+// O = A + 1 outputs as a template argument (the rows live in registers): every Atari action
+// set, A = 2..18 (the full ALE set is 18; Breakout 4, Pong 6, Ms. Pac-Man 9)
+template <class F>
+static int heads_dispatch(int O, F&& f) {
+    switch (O) {
+#define FI_HEADS_CASE(o) case o: return f(std::integral_constant<int, o>{});
+        FI_HEADS_CASE(3) FI_HEADS_CASE(4) FI_HEADS_CASE(5) FI_HEADS_CASE(6) FI_HEADS_CASE(7)
+        FI_HEADS_CASE(8) FI_HEADS_CASE(9) FI_HEADS_CASE(10) FI_HEADS_CASE(11) FI_HEADS_CASE(12)
+        FI_HEADS_CASE(13) FI_HEADS_CASE(14) FI_HEADS_CASE(15) FI_HEADS_CASE(16) FI_HEADS_CASE(17)
+        FI_HEADS_CASE(18) FI_HEADS_CASE(19)
+#undef FI_HEADS_CASE
+        default: return fail(FI_ERR_INVALID, "atari heads: A + 1 = " + std::to_string(O) + " outside [3, 19]");
+    }
+}
+
+static int heads_wgrad_launch(int O, const float* dlog, const float* dval, const __bf16* h, float* slab, float* cs,
+                              int R, int TB, hipStream_t s) {
+    FI_TRY(heads_dispatch(O, [&](auto o) {
+        hipLaunchKernelGGL(heads_wgrad_valu<decltype(o)::value>, dim3(kHeadsGrid), dim3(256), 0, s, dlog, dval, h,
+                           slab, cs, R, TB);
+        return FI_OK;
+    }));
     FI_HIP_CHECK(hipGetLastError());
     return FI_OK;
 }
 
-constexpr int kHeadsDgradGrid = 1024;
-static int heads_dgrad_launch(const float* dlog, const float* dval, const float* wh, const __bf16* h, __bf16* dh,
-                              int R, int TB, float* fcb_slab, hipStream_t s) {
-    hipLaunchKernelGGL(heads_dgrad_valu<19>, dim3(kHeadsDgradGrid), dim3(256), 0, s, dlog, dval, wh, h, dh, R, TB,
-                       fcb_slab);
+static int heads_dgrad_launch(int O, const float* dlog, const float* dval, const float* wh, const __bf16* h,
+                              __bf16* dh, int R, int TB, float* fcb_slab, hipStream_t s) {
+    FI_TRY(heads_dispatch(O, [&](auto o) {
+        hipLaunchKernelGGL(heads_dgrad_valu<decltype(o)::value>, dim3(kHeadsDgradGrid), dim3(256), 0, s, dlog,
+                           dval, wh, h, dh, R, TB, fcb_slab);
+        return FI_OK;
+    }));
     FI_HIP_CHECK(hipGetLastError());
     return FI_OK;
 }
@@ -669,15 +624,15 @@ static int heads_dgrad_launch(const float* dlog, const float* dval, const float*
 // ------------------------------------------------------------------ weight layouts (bf16)
 struct WeightsBf16 {
     __bf16 *c1T, *c2T, *c3T, *fcT, *hT;  // forward B operands [out][k]
-    __bf16 *c2D, *c3D, *fcB, *hD;        // dgrad B operands
+    __bf16 *c2D, *c3D, *fcB;             // dgrad B operands
 };
 
 __global__ void weights_bf16_kernel(const float* __restrict__ p, Offsets o, int A, WeightsBf16 w) {
     const int O = A + 1;
     // segment sizes
     const size_t n1 = 32 * 256, n2 = 64 * 512, n3 = 64 * 576, nf = (size_t)512 * 3136,
-                 nh = 32 * 512, n2d = 4 * 32 * 256, n3d = 64 * 576, nfb = nf, nhd = 512 * 32;
-    const size_t total = n1 + n2 + n3 + nf + nh + n2d + n3d + nfb + nhd;
+                 nh = 32 * 512, n2d = 4 * 32 * 256, n3d = 64 * 576, nfb = nf;
+    const size_t total = n1 + n2 + n3 + nf + nh + n2d + n3d + nfb;
     for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < total;
          t += (size_t)gridDim.x * blockDim.x) {
         size_t i = t;
@@ -705,9 +660,7 @@ __global__ void weights_bf16_kernel(const float* __restrict__ p, Offsets o, int 
             continue;
         }
         i -= n3d;
-        if (i < nfb) { w.fcB[i] = (__bf16)p[o.fcw + i]; continue; }
-        i -= nfb;
-        { const int j = i / 32, oo = i % 32; w.hD[i] = (__bf16)(oo < O ? p[o.hw + (size_t)j * O + oo] : 0.f); }
+        w.fcB[i] = (__bf16)p[o.fcw + i];
     }
 }
 
@@ -764,14 +717,14 @@ static bool dmalloc(AtariImpl* I, T** p, size_t n) {
 }
 
 // split factors (blocks over the reduction) per weight-gradient GEMM
-constexpr int SPL_H = 128, SPL_FC = 9, SPL_C3 = 160, SPL_C2 = 256, SPL_C1 = 512;
+constexpr int SPL_FC = 9, SPL_C3 = 160, SPL_C2 = 256, SPL_C1 = 512;
 // the fused conv2 backward + conv1 weight gradient's slabs: conv2 [grid][512][64], then conv1
 // [grid][kC1Segs][256][32] (kC1Segs: atari.h, shared with atari_fr.hip's writer)
 constexpr int GBM = 128;  // M-tile of the dgrad GEMMs (class stride granularity)
 
 AtariNet* atari_create(int B, int T, int A) {
-    if (A + 1 > geo::HP) {
-        set_error("atari: A+1 must be <= 32");
+    if (A < 2 || A > 18) {  // the heads backward keeps a row of A + 1 outputs in registers
+        set_error("atari: 2 <= A <= 18 (the full ALE action set is 18)");
         return nullptr;
     }
     AtariNet* n = new AtariNet();
@@ -796,11 +749,10 @@ AtariNet* atari_create(int B, int T, int A) {
               dmalloc(I, &I->wb.c1T, 32 * 256) && dmalloc(I, &I->wb.c2T, 64 * 512) &&
               dmalloc(I, &I->wb.c3T, 64 * 576) && dmalloc(I, &I->wb.fcT, (size_t)512 * 3136) &&
               dmalloc(I, &I->wb.hT, 32 * 512) && dmalloc(I, &I->wb.c2D, 4 * 32 * 256) &&
-              dmalloc(I, &I->wb.c3D, 64 * 576) && dmalloc(I, &I->wb.fcB, (size_t)3136 * 512) &&
-              dmalloc(I, &I->wb.hD, 512 * 32);
+              dmalloc(I, &I->wb.c3D, 64 * 576) && dmalloc(I, &I->wb.fcB, (size_t)3136 * 512);
     const size_t s_fc = (size_t)SPL_FC * 3136 * 512, s_c3 = (size_t)SPL_C3 * 576 * 64,
                  s_c2 = (size_t)SPL_C2 * (512 * 64 + kC1Segs * 256 * 32), s_c1 = (size_t)SPL_C1 * 256 * 32,
-                 s_h = (size_t)SPL_H * 512 * 32;
+                 s_h = (size_t)kHeadsGrid * 512 * 19;  // heads_wgrad_valu's [grid][512][O]
     I->slab_floats = std::max(std::max(s_fc, s_c3), std::max(std::max(s_c2, s_c1), s_h)) + 1024 * 512;
     ok = ok && dmalloc(I, &I->slab, I->slab_floats);
     if (!ok) {
@@ -904,26 +856,16 @@ int atari_backward(AtariNet* n, const uint8_t* frames, const float* dlogits, con
     using namespace geo;
     float* slab = I->slab;
     float* cs = I->slab + I->slab_floats - 1024 * 512;
-    DoutRows dout{dlogits, dvalue, N, I->TB, A};
     int rc;
 #define FI_A(tag, x) do { TagScope ts_(tg, tag); rc = (x); if (rc) return rc; } while (0)
-    // heads: wgrad [512][O] + bias, dgrad -> dh (masked by h)
-    if (O == 19) {  // packed-fp32 VALU kernels (A = 18, the configured action set)
-        FI_A("heads_wgrad", heads_wgrad_launch(dlogits, dvalue, I->h, slab, cs, Nb, I->TB, s));
-        FI_A("reduce_slabs", reduce_slabs(slab, kHeadsGrid, (size_t)FCO * O, grads + o.hw, s));
-        FI_A("reduce_slabs", reduce_slabs(cs, kHeadsGrid, (size_t)O, grads + o.hb, s));
-        // heads dgrad also leaves the fc bias partials (column sums of dh) in the slab
-        FI_A("heads_dgrad", heads_dgrad_launch(dlogits, dvalue, I->params + o.hw, I->h, I->dh, Nb, I->TB, slab, s));
-        FI_A("reduce_slabs", reduce_slabs(slab, kHeadsDgradGrid, (size_t)FCO, grads + o.fcb, s));
-    } else {
-        FI_A("heads_wgrad", (wgrad<128, 32, 4, 1>(RowsBf16{I->h, N, FCO}, dout, slab, cs, N, FCO, O, SPL_H, 1.f, s)));
-        FI_A("reduce_slabs", reduce_slabs(slab, SPL_H, (size_t)FCO * O, grads + o.hw, s));
-        FI_A("reduce_slabs", reduce_slabs(cs, SPL_H, (size_t)O, grads + o.hb, s));
-        FI_A("heads_dgrad", (gemm<128, 128, 2, 2>(dout, RowsBf16{I->wb.hD, FCO, HP}, EpiMaskBf16{I->dh, I->h, FCO}, N, FCO,
-                                   HP, s)));
-        FI_A("fc_bias", colsum_bf16(I->dh, N, FCO, slab, s));
-        FI_A("reduce_slabs", reduce_slabs(slab, kColsumSplits, (size_t)FCO, grads + o.fcb, s));
-    }
+    // heads: wgrad [512][O] + bias, dgrad -> dh (masked by h), both packed-fp32 VALU kernels
+    // (K = A + 1 <= 19 is too thin for MFMA); the dgrad also leaves the fc bias partials
+    // (column sums of dh) in the slab
+    FI_A("heads_wgrad", heads_wgrad_launch(O, dlogits, dvalue, I->h, slab, cs, Nb, I->TB, s));
+    FI_A("reduce_slabs", reduce_slabs(slab, kHeadsGrid, (size_t)FCO * O, grads + o.hw, s));
+    FI_A("reduce_slabs", reduce_slabs(cs, kHeadsGrid, (size_t)O, grads + o.hb, s));
+    FI_A("heads_dgrad", heads_dgrad_launch(O, dlogits, dvalue, I->params + o.hw, I->h, I->dh, Nb, I->TB, slab, s));
+    FI_A("reduce_slabs", reduce_slabs(slab, kHeadsDgradGrid, (size_t)FCO, grads + o.fcb, s));
     // fc: wgrad [3136][512] + bias, dgrad -> da3 (masked by a3)
     // fc: wgrad (fc_gemm.hip) as fp32 slabs reduced into the gradient blob, bias = column
     // sums of dh (left by heads dgrad), dgrad -> da3 unmasked (conv3's backward applies the

@@ -68,12 +68,13 @@ int fc_wgrad_splits(int rows);  // R-slices (fp32 slabs of 3136 x 512) fc_wgrad_
 int fc_wgrad_launch(const __bf16* a3, const __bf16* dh, float* slab, float* dw, int rows, hipStream_t s);
 int reduce_slabs(float* slab, int splits, size_t count, float* out, hipStream_t s);  // slab is scratch (overwritten)
 // squared L2 norm of g -> *out; optionally also sums vt_nblk V-trace loss partials [i][3]
-// into vt_losses[0..2] in the same (final) launch
+// into vt_losses[0..2] in the same (final) launch; *nonfinite = 1 when the norm is NaN / Inf
 int grad_sqnorm(const float* g, size_t n, double* part, int nblk, double* out, hipStream_t s,
-                const double* vt_part = nullptr, int vt_nblk = 0, double* vt_losses = nullptr);
+                const double* vt_part = nullptr, int vt_nblk = 0, double* vt_losses = nullptr,
+                int* nonfinite = nullptr);
 int optimizer_step(int opt, float* p, const float* g, float* m, float* v, size_t n, float lr,
                    float b1, float b2, float eps, double bc1, double bc2, const double* sqnorm,
-                   float max_norm, hipStream_t s, const int* skip = nullptr);
+                   float max_norm, hipStream_t s, const int* skip = nullptr);  // skip: int[2], see misc.hip
 int to_bf16(const float* src, uint16_t* dst, size_t n, hipStream_t s);
 int fill_hash_bf16(void* dst, size_t n, uint32_t seed, hipStream_t s);
 int synth_launch(uint64_t seed, int T, int B, int B_glob, int b_off, int A, int D, float gamma,

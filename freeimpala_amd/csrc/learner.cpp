@@ -522,18 +522,24 @@ static int mlp_backward(fi_learner* l, GradReadyHook* gr) {
 // parameters and moments untouched, and the step reports FI_ERR_INVALID once it has
 // completed (the oracle rejects the same batch, oracle/impala_oracle.c). Called after the
 // stream has been synchronised.
+// bad[0]: out-of-range actions (all-reduced); bad[1]: the gradient norm was NaN / Inf. The norm
+// is taken from the all-reduced gradient, so every replica sees the same value and skips the
+// same update (both flags are read by the optimizer kernels, misc.hip).
 static int check_rejected(fi_learner* l) {
-    int bad = 0;
-    FI_HIP_CHECK(hipMemcpy(&bad, l->bad, sizeof(int), hipMemcpyDeviceToHost));
-    if (bad == 0) return FI_OK;
+    int bad[2] = {0, 0};
+    FI_HIP_CHECK(hipMemcpy(bad, l->bad, sizeof(bad), hipMemcpyDeviceToHost));
+    if (bad[0] == 0 && bad[1] == 0) return FI_OK;
     l->step_count--;
     l->version--;
+    if (bad[0] == 0)
+        return fail(FI_ERR_NONFINITE, "step: the gradient norm is not finite (NaN / Inf in the "
+                                      "batch's losses or gradients); update skipped, parameters unchanged");
     if (l->comm && l->nranks > 1)
-        return fail(FI_ERR_INVALID, "step: " + std::to_string(bad) + " action(s) outside [0, " +
+        return fail(FI_ERR_INVALID, "step: " + std::to_string(bad[0]) + " action(s) outside [0, " +
                                         std::to_string(l->A) + ") in the data-parallel group's batch "
                                         "(all-reduced reject flag); batch rejected on every replica, "
                                         "parameters unchanged");
-    return fail(FI_ERR_INVALID, "step: " + std::to_string(bad) + " action(s) outside [0, " +
+    return fail(FI_ERR_INVALID, "step: " + std::to_string(bad[0]) + " action(s) outside [0, " +
                                     std::to_string(l->A) + ") in the batch; batch rejected, "
                                     "parameters unchanged");
 }
@@ -604,7 +610,7 @@ static int run_step(fi_learner* l, bool have_host_batch, fi_step_stats* out) {
     {
         Tag t(l, "grad_norm");  // + the V-trace loss sums (losses land in small[0..2])
         FI_TRY(grad_sqnorm(l->grads, l->nparams, l->small + 8, kSqParts, l->small + 3, l->stream,
-                           vtrace_partials(l->vt_ws), vt_nblk, l->small));
+                           vtrace_partials(l->vt_ws), vt_nblk, l->small, l->bad + 1));
     }
     const int step = l->step_count + 1;
     const double bc1 = 1.0 - std::pow((double)l->cfg.beta1, step);

@@ -280,7 +280,7 @@ __global__ void sqnorm_part_kernel(const float* __restrict__ g, size_t n, double
 }
 
 __global__ void sqnorm_final_kernel(const double* part, int nblk, double* out, const double* vt_part,
-                                    int vt_nblk, double* vt_losses) {
+                                    int vt_nblk, double* vt_losses, int* nonfinite) {
     __shared__ double red[4][4];
     double s = 0.0, l0 = 0.0, l1 = 0.0, l2 = 0.0;
     for (int i = threadIdx.x; i < nblk; i += blockDim.x) s += part[i];
@@ -303,16 +303,21 @@ __global__ void sqnorm_final_kernel(const double* part, int nblk, double* out, c
     if (threadIdx.x < 4) {
         const double* r = red[threadIdx.x];
         const double v = (r[0] + r[1]) + (r[2] + r[3]);
-        if (threadIdx.x == 0) *out = v;
-        else if (vt_losses) vt_losses[threadIdx.x - 1] = v;
+        if (threadIdx.x == 0) {
+            *out = v;
+            // squares of finite fp32 values summed in fp64 cannot overflow: a non-finite norm
+            // means a NaN / Inf gradient element
+            if (nonfinite)  // exponent all ones: Inf or NaN (a bit test, immune to fast-math folding)
+                *nonfinite = (__double_as_longlong(v) & 0x7FF0000000000000LL) == 0x7FF0000000000000LL;
+        } else if (vt_losses) vt_losses[threadIdx.x - 1] = v;
     }
 }
 
 int grad_sqnorm(const float* g, size_t n, double* part, int nblk, double* out, hipStream_t s,
-                const double* vt_part, int vt_nblk, double* vt_losses) {
+                const double* vt_part, int vt_nblk, double* vt_losses, int* nonfinite) {
     hipLaunchKernelGGL(sqnorm_part_kernel, dim3(nblk), dim3(256), 0, s, g, n, part);
     hipLaunchKernelGGL(sqnorm_final_kernel, dim3(1), dim3(256), 0, s, part, nblk, out, vt_part,
-                       vt_losses ? vt_nblk : 0, vt_losses);
+                       vt_losses ? vt_nblk : 0, vt_losses, nonfinite);
     FI_HIP_CHECK(hipGetLastError());
     return FI_OK;
 }
@@ -322,7 +327,9 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                             float* __restrict__ m, float* __restrict__ v, size_t n, float lr,
                             float b1, float b2, float eps, double bc1, double bc2,
                             const double* sqnorm, float max_norm, const int* skip) {
-    if (skip && *skip != 0) return;  // rejected batch: parameters and moments stay as they are
+    // skip[0]: rejected batch (bad actions), skip[1]: non-finite gradient norm -- parameters
+    // and moments stay as they are
+    if (skip && (skip[0] | skip[1]) != 0) return;
     float scale = 1.f;
     if (max_norm > 0.f) {
         const double norm = sqrt(*sqnorm);
@@ -342,7 +349,7 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
 
 __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, size_t n, float lr,
                            const double* sqnorm, float max_norm, const int* skip) {
-    if (skip && *skip != 0) return;
+    if (skip && (skip[0] | skip[1]) != 0) return;
     float scale = 1.f;
     if (max_norm > 0.f) {
         const double norm = sqrt(*sqnorm);

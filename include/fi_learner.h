@@ -35,7 +35,8 @@ enum fi_status {
     FI_ERR_OOM = -3,         /* device or pinned allocation failed                   */
     FI_ERR_STATE = -4,       /* call not valid in the current state                  */
     FI_ERR_COMM = -5,        /* RCCL failure                                         */
-    FI_ERR_UNSUPPORTED = -6  /* configuration not built                              */
+    FI_ERR_UNSUPPORTED = -6, /* configuration not built                              */
+    FI_ERR_NONFINITE = -7    /* NaN / Inf in the (all-reduced) gradient: update skipped */
 };
 
 enum fi_arch { FI_ARCH_MLP = 0, FI_ARCH_ATARI = 1 };
@@ -57,7 +58,7 @@ typedef struct fi_learner_config {
     int32_t arch;             /* fi_arch                                              */
     int32_t seq_len;          /* T  (--seq-length)                                    */
     int32_t batch;            /* B  per device (--batch-size / number of GPUs)        */
-    int32_t num_actions;      /* A  (<= 64)                                           */
+    int32_t num_actions;      /* A: 2..64 (MLP), 2..18 (Atari: the ALE action sets)   */
     int32_t obs_dim;          /* MLP observation width (128)                          */
     int32_t hidden;           /* MLP hidden width (256)                               */
     int32_t optimizer;        /* fi_optimizer                                         */

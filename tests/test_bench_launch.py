@@ -95,7 +95,7 @@ def _timed_worker(rank, world, port, out_dir):
     from freeimpala_amd import launch
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        delay = 0.01 if rank == 0 else 0.05
+        delay = 0.01 if rank == 0 else 0.15
         own, br = launch.timed_steps(lambda: time.sleep(delay), lambda: None, dist.barrier, 4)
         per = launch.gather_objects({"ms_per_step": 1000 * own / 4, "allreduce_ms": 0.0})
         dp = launch.data_parallel_fields(per, grad_bytes=16, buckets=None)
@@ -111,8 +111,9 @@ def test_rank_own_time_excludes_the_wait_for_the_slowest_rank(tmp_path):
     mp.start_processes(_timed_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True,
                        start_method="spawn")
     t = [json.load(open(tmp_path / f"t{r}.json")) for r in range(2)]
-    assert t[0]["own"] < 0.12 and t[1]["own"] >= 0.2   # 4 x 10 ms vs 4 x 50 ms
-    assert t[0]["bracketed"] >= 0.2                     # rank 0's bracket waits for rank 1
+    # 4 x 10 ms vs 4 x 150 ms (margins wide enough for a loaded CI host)
+    assert t[0]["own"] < 0.3 and t[1]["own"] >= 0.6
+    assert t[0]["bracketed"] >= 0.6                     # rank 0's bracket waits for rank 1
     per = t[0]["dp"]["rank_ms_per_step"]["per_rank"]
     assert per[1] > 2 * per[0]
 

@@ -182,6 +182,40 @@ def test_atari_fc_path_parity(orc, T, B, grid, monkeypatch):
     L.close()
 
 
+@pytest.mark.parametrize("A", [4, 6, 9])
+def test_atari_production_path_other_action_counts(orc, A, monkeypatch):
+    """Atari minimal action sets other than the full 18 (Breakout 4, Pong 6, Ms. Pac-Man 9):
+    the heads then run on the generic MFMA GEMM / weight-gradient kernels instead of the
+    packed-fp32 VALU pair built for A = 18, beside the production conv and fc kernels. Every
+    stage and gradient against the oracle, the persistent grid shrunk so workgroups walk
+    several frames."""
+    for k in ("FI_KEEP_DA1", "FI_A1_NHWC", "FI_FWD_UNFUSED", "FI_BWD_UNFUSED"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("FI_FR_GRID", "5")
+    T, B = 2, 16
+    N = (T + 1) * B
+    monkeypatch.setenv("FI_KEEP_DA1", "1")
+    twin = mk(T=T, B=B, A=A, seed=23)
+    monkeypatch.delenv("FI_KEEP_DA1")
+    L = mk(T=T, B=B, A=A, seed=23)
+    for x in (twin, L):
+        x.synth(seed=31 * A)
+    twin.step_resident()
+    da1 = bf16_to_f32(twin.tensor("da1", np.uint16, (N, 20, 20, 32)))
+    g = _check_step_against_oracle(orc, L, T, B, A, a1_planar=True, da1=da1)
+    np.testing.assert_array_equal(g, twin.tensor("grads"))
+    twin.close()
+    L.close()
+
+
+def test_atari_action_set_limit():
+    """The heads backward keeps a row of A + 1 outputs in registers, instantiated for every
+    ALE action set (A <= 18); a larger A is refused at creation, not run on another path."""
+    from freeimpala_amd._abi import FiError
+    with pytest.raises(FiError, match="A <= 18"):
+        mk(A=19)
+
+
 def test_atari_training_reduces_loss():
     """gamma = 0 makes the V-trace target the (clipped) immediate reward, so the value loss of a
     fixed batch is a plain regression that SGD must reduce."""

@@ -405,6 +405,46 @@ def test_rejected_batch_under_comm_leaves_state_unchanged(orc, monkeypatch, atta
     R.close()
 
 
+@pytest.mark.parametrize("attach", [None, "uid"])
+@pytest.mark.parametrize("poison", [np.nan, np.inf])
+def test_nonfinite_gradient_skips_update(orc, monkeypatch, attach, poison):
+    """A NaN / Inf reward (a corrupt record) makes the losses and the summed gradient
+    non-finite. The gradient-norm kernel flags it (the norm is taken from the all-reduced
+    gradient, so every replica sees the same flag) and the optimizer skips the update: the
+    step returns FI_ERR_NONFINITE (-7), parameters, both Adam moments and the version stay
+    bit-unchanged, and the next good batch matches a handle that never saw the bad one. Sync
+    and async forms; with and without the in-step all-reduce path (one-rank communicator)."""
+    from freeimpala_amd._abi import FiError
+    from freeimpala_amd.learner import DeviceLearner, pack_records
+    monkeypatch.setenv("FI_COMM_SINGLE", "1")
+    T, B = 4, 32
+    good = orc.synth_batch(47, T=T, B=B, A=18, D=128)
+    bad = {k: (None if v is None else v.copy()) for k, v in good.items()}
+    bad["rewards"][1, 7] = poison
+    pk = lambda b: pack_records(b["obs"], b["mu"], b["actions"], b["rewards"], b["discounts"],
+                                entry_size=T + 1)
+    L, R = mk(T=T, B=B, seed=6, optimizer="adam"), mk(T=T, B=B, seed=6, optimizer="adam")
+    if attach:
+        L.attach_comm(DeviceLearner.comm_unique_id(), 0, 1)
+    L.step(pk(good))
+    R.step(pk(good))
+    p1, m1, v1 = L.get_params(), L.tensor("adam_m"), L.tensor("adam_v")
+    with pytest.raises(FiError, match=r"rc=-7.*not finite"):
+        L.step(pk(bad))
+    L.step_async(pk(bad))
+    with pytest.raises(FiError, match="not finite"):
+        L.wait()
+    np.testing.assert_array_equal(L.get_params(), p1)
+    np.testing.assert_array_equal(L.tensor("adam_m"), m1)
+    np.testing.assert_array_equal(L.tensor("adam_v"), v1)
+    s, r = L.step(pk(good)), R.step(pk(good))
+    assert s["version"] == r["version"] == 2
+    assert np.isfinite(s["grad_norm"]) and s["total_loss"] == r["total_loss"]
+    np.testing.assert_array_equal(L.get_params(), R.get_params())
+    L.close()
+    R.close()
+
+
 def _two_devices():
     from freeimpala_amd import hip
     n = hip.device_count()
