@@ -102,6 +102,33 @@ def test_mlp_step_parity(orc, T, B):
     assert st["version"] == 1
 
 
+@pytest.mark.parametrize("D,H,A,T,B", [(17, 48, 4, 3, 24), (1, 5, 2, 2, 16), (128, 1000, 33, 2, 40),
+                                       (64, 512, 64, 3, 16), (100, 130, 7, 4, 8)])
+def test_mlp_other_shapes_parity(orc, D, H, A, T, B):
+    """MLP shapes away from config #2 (every obs_dim / hidden / action count the create call
+    accepts is a legal configuration): odd widths that cut the fp32 MFMA tiles (hidden 5, 48,
+    130, 1000), a one-float observation, A up to the 64-action limit, B not a multiple of 16.
+    Forward, V-trace, every gradient and the SGD update against the oracle."""
+    L = mk(T=T, B=B, A=A, D=D, H=H)
+    L.synth(seed=D * 7 + H)
+    batch = orc.synth_batch(D * 7 + H, T=T, B=B, A=A, D=D)
+    p0 = L.get_params()
+    st = L.step_resident()
+    ref = oracle_step(orc, L, batch, p0)
+    scaled_close(L.tensor("logits", shape=(T + 1, B, A)), ref["logits"], what="logits")
+    scaled_close(L.tensor("values", shape=(T + 1, B)), ref["values"], what="values")
+    scaled_close(L.tensor("dlogits", shape=(T, B, A)), ref["vt"]["dlogits"], what="dlogits")
+    g = L.tensor("grads")
+    off = np.cumsum([0, D * H, H, H * H, H, H * (A + 1), A + 1])
+    assert g.size == off[-1]
+    for i, name in enumerate(["W1", "b1", "W2", "b2", "Wh", "bh"]):
+        grads_close(g[off[i]:off[i + 1]], ref["grads"][off[i]:off[i + 1]], what=name)
+    tot = orc.total_loss(ref["vt"]["losses"])
+    assert abs(st["total_loss"] - tot) <= 1e-5 * max(1.0, abs(tot))
+    scaled_close(L.get_params(), p0 - np.float32(1e-3) * g, 1e-6, "sgd update")
+    L.close()
+
+
 def test_mlp_config2_full_size(orc):
     """Config #2: T=100, B=512, A=18, obs 128, MLP 128-256-256, fp32 numerics vs the oracle."""
     T, B = 100, 512
