@@ -8,6 +8,10 @@ cd "$(dirname "$0")/.."
 n=$1; shift
 SRC=${SRC:-freeimpala_amd/csrc/atari_fr.hip}
 base=$(basename "$SRC")
+case " farmer.hip vtrace.hip gemm_f32.hip misc.hip atari.hip atari_fr.hip fc_gemm.hip learner.cpp " in
+  *" $base "*) ;;
+  *) echo "build_exp.sh: $SRC must be named after the product source it replaces" >&2; exit 2 ;;
+esac
 mkdir -p build/ab
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Iinclude -Ifreeimpala_amd/csrc \
   -Wno-unused-result -Wno-unused-value -munsafe-fp-atomics "$@" -x hip -c "$SRC" -o build/ab/x_$n.o
