@@ -10,6 +10,12 @@
 //       record schema) from the same parameters; checks the two results are identical,
 //       then writes the batch, the parameters and the step statistics to OUT_DIR so that
 //       tests/test_host_cpp.py can compare them with the CPU oracle.
+//   host_learner_check pipeline
+//       one player at B = 1344, T = 100 (139 MB per batch: the library copies it with its
+//       parallel staging threads), three asynchronous steps back to back (pinned double
+//       buffering, H2D on the copy stream beside the previous step) against the same three
+//       steps taken synchronously on a twin handle: identical parameters. Built under
+//       ThreadSanitizer with the library's host side instrumented (tests/cpp/tsan.mk).
 //   host_learner_check worker_fail DIR
 //       freeimpala_amd::Learner whose staging acquisition fails (a test subclass): the worker
 //       must stop, report workerFailed(), and drain its buffer so an actor blocked in write() on
@@ -195,6 +201,41 @@ static int gpu_mode(const std::string& out) {
     return 0;
 }
 
+static int pipeline_mode() {
+    LearnerConfig c;
+    c.players = 2;  // player 0 asynchronous, player 1 its synchronous twin
+    c.batch_size = 1344;  // 139 MB per batch: 3 staging copy threads (one per 64 MiB, csrc/learner.cpp)
+    c.seq_length = 100;
+    c.entry_size = 101;
+    c.optimizer = "adam";
+    DeviceLearner L(c);
+    const int T = (int)c.seq_length, A = c.num_actions, D = c.obs_dim;
+    std::vector<std::vector<std::vector<char>>> batches;
+    for (int k = 0; k < 3; ++k) {
+        auto b = make_batch(c.batch_size, c.entry_records(), T, A, D);
+        for (auto& e : b) e[772] ^= (char)k;  // distinct rewards per batch
+        batches.push_back(std::move(b));
+    }
+    std::vector<char> p0;
+    uint64_t v0 = 0;
+    CHECK(L.publish(0, p0, v0) && L.load(1, p0, v0));
+    std::atomic<bool> twin_ok{true};
+    std::thread twin([&] {
+        for (const auto& b : batches)
+            if (!L.step(1, b)) twin_ok = false;
+    });
+    for (const auto& b : batches) CHECK(L.step_async(0, b));
+    CHECK(L.wait(0));
+    twin.join();
+    CHECK(twin_ok.load());
+    std::vector<char> pa, pb;
+    uint64_t va = 0, vb = 0;
+    CHECK(L.publish(0, pa, va) && L.publish(1, pb, vb));
+    CHECK(va == v0 + 3 && vb == v0 + 3 && pa == pb && pa != p0);
+    std::printf("OK pipeline\n");
+    return 0;
+}
+
 struct FailingLearner : freeimpala_amd::Learner {
     using freeimpala_amd::Learner::Learner;
     std::atomic<int> calls{0};
@@ -236,11 +277,12 @@ int main(int argc, char** argv) {
     try {
         if (mode == "cpu") return cpu_mode();
         if (mode == "gpu" && argc > 2) return gpu_mode(argv[2]);
+        if (mode == "pipeline") return pipeline_mode();
         if (mode == "worker_fail" && argc > 2) return worker_fail_mode(argv[2]);
     } catch (const std::exception& e) {
         std::fprintf(stderr, "unexpected exception: %s\n", e.what());
         return 1;
     }
-    std::fprintf(stderr, "usage: host_learner_check cpu | gpu OUT_DIR\n");
+    std::fprintf(stderr, "usage: host_learner_check cpu | gpu OUT_DIR | pipeline | worker_fail DIR\n");
     return 2;
 }

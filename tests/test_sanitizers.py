@@ -117,16 +117,23 @@ def _tsan_env():
 @pytest.mark.skipif(not os.path.exists(os.path.join(TSAN_BIN, "host_learner_check")),
                     reason="build/tsan not built (make -f tests/cpp/tsan.mk)")
 def test_device_host_paths_race_free_under_tsan(tmp_path):
-    """The host side of the DEVICE learner under ThreadSanitizer on the GPU (the ROCm runtime,
-    uninstrumented, is suppressed: its own thread synchronisation is invisible to TSAN):
+    """The host side of the DEVICE learner under ThreadSanitizer on the GPU, the library's own
+    host code (csrc/learner.cpp) instrumented too (build/tsan/lib, tests/cpp/tsan.mk); the ROCm
+    runtime, uninstrumented, is suppressed (its own thread synchronisation is invisible to TSAN):
       * tests/cpp/host_learner_check.cpp gpu -- two players stepping concurrently through the
         C ABI from their own threads (DeviceLearner, pinned staging, async H2D);
+      * host_learner_check pipeline -- 139 MB batches copied by the library's staging threads,
+        three asynchronous steps back to back beside a synchronous twin on another thread;
       * build/fi_freeimpala with the device learner -- 2 players, 4 actor threads, the
         BasicLearner worker and checkpoint threads, model sync, stop()."""
     r = subprocess.run([os.path.join(TSAN_BIN, "host_learner_check"), "gpu", str(tmp_path / "hlc")],
                        capture_output=True, text=True, timeout=300, env=_tsan_env())
     assert "WARNING: ThreadSanitizer" not in r.stderr, r.stderr[-6000:]
     assert r.returncode == 0 and "OK gpu" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-3000:])
+    r = subprocess.run([os.path.join(TSAN_BIN, "host_learner_check"), "pipeline"],
+                       capture_output=True, text=True, timeout=300, env=_tsan_env())
+    assert "WARNING: ThreadSanitizer" not in r.stderr, r.stderr[-6000:]
+    assert r.returncode == 0 and "OK pipeline" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-3000:])
     r = subprocess.run([os.path.join(TSAN_BIN, "fi_freeimpala"), "--players", "2", "--iterations", "32",
                         "--buffer-capacity", "32", "--batch-size", "16", "--seq-length", "20", "--agents", "4",
                         "--entry-size", "42", "--game-steps", "42", "--agent-time", "0", "--checkpoint-freq", "2",
@@ -134,3 +141,31 @@ def test_device_host_paths_race_free_under_tsan(tmp_path):
                        capture_output=True, text=True, timeout=300, env=_tsan_env())
     assert "WARNING: ThreadSanitizer" not in r.stderr, r.stderr[-6000:]
     assert r.returncode == 0 and '"learner_iterations": [8, 8]' in r.stdout, (r.returncode, r.stderr[-3000:])
+
+
+ASAN_BIN = os.path.join(ROOT, "build", "asan")
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(os.path.join(ASAN_BIN, "host_learner_check")),
+                    reason="build/asan not built (make -f tests/cpp/tsan.mk)")
+def test_device_host_paths_clean_under_asan_ubsan(tmp_path):
+    """The same device host paths under AddressSanitizer + UBSan, the library's host side
+    (csrc/learner.cpp) instrumented as well (build/asan/lib): two players stepping concurrently,
+    the pipelined 139 MB batches through the staging threads, and the threaded CLI on the device
+    learner. Every finding is fatal; leak checking is off (the ROCm runtime holds its
+    allocations to process exit), and the link-order check is off (the harness preloads a
+    library of its own ahead of the sanitizer runtime)."""
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:verify_asan_link_order=0:abort_on_error=0",
+               UBSAN_OPTIONS="print_stacktrace=1")
+    (tmp_path / "hlc").mkdir()
+    runs = [[os.path.join(ASAN_BIN, "host_learner_check"), "gpu", str(tmp_path / "hlc")],
+            [os.path.join(ASAN_BIN, "host_learner_check"), "pipeline"],
+            [os.path.join(ASAN_BIN, "fi_freeimpala"), "--players", "2", "--iterations", "32",
+             "--buffer-capacity", "32", "--batch-size", "16", "--seq-length", "20", "--agents", "4",
+             "--entry-size", "42", "--game-steps", "42", "--agent-time", "0", "--checkpoint-freq", "2",
+             "--checkpoint-location", str(tmp_path / "ck")]]
+    for cmd in runs:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+        assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-6000:]
+        assert r.returncode == 0, (cmd[1:2], r.returncode, r.stdout[-2000:], r.stderr[-3000:])
