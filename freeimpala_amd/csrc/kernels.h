@@ -74,7 +74,7 @@ int grad_sqnorm(const float* g, size_t n, double* part, int nblk, double* out, h
                 int* nonfinite = nullptr);
 int optimizer_step(int opt, float* p, const float* g, float* m, float* v, size_t n, float lr,
                    float b1, float b2, float eps, double bc1, double bc2, const double* sqnorm,
-                   float max_norm, hipStream_t s, const int* skip = nullptr);  // skip: int[2], see misc.hip
+                   float max_norm, hipStream_t s, int* skip = nullptr);  // skip: int[4], see misc.hip
 int to_bf16(const float* src, uint16_t* dst, size_t n, hipStream_t s);
 int fill_hash_bf16(void* dst, size_t n, uint32_t seed, hipStream_t s);
 int synth_launch(uint64_t seed, int T, int B, int B_glob, int b_off, int A, int D, float gamma,

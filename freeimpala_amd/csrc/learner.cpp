@@ -522,26 +522,32 @@ static int mlp_backward(fi_learner* l, GradReadyHook* gr) {
 // parameters and moments untouched, and the step reports FI_ERR_INVALID once it has
 // completed (the oracle rejects the same batch, oracle/impala_oracle.c). Called after the
 // stream has been synchronised.
-// bad[0]: out-of-range actions (all-reduced); bad[1]: the gradient norm was NaN / Inf. The norm
-// is taken from the all-reduced gradient, so every replica sees the same value and skips the
-// same update (both flags are read by the optimizer kernels, misc.hip).
+// The flag words l->bad (csrc/misc.hip, skip_update): [0] out-of-range actions of the current
+// step (all-reduced), [1] its gradient norm was NaN / Inf (taken from the all-reduced gradient,
+// so every replica sees the same value), [2] updates skipped since the last check, [3] their
+// reasons (1 = actions, 2 = non-finite). Every replica skips the same updates. A synchronous
+// step checks its own; fi_learner_wait checks every step enqueued since the last check, so a
+// skipped step behind others still in flight is reported, and the version counts applied
+// updates only (an enqueued step behind a skipped one keeps the Adam step number it was given).
 static int check_rejected(fi_learner* l) {
-    int bad[2] = {0, 0};
+    int bad[4] = {0, 0, 0, 0};
     FI_HIP_CHECK(hipMemcpy(bad, l->bad, sizeof(bad), hipMemcpyDeviceToHost));
-    if (bad[0] == 0 && bad[1] == 0) return FI_OK;
-    l->step_count--;
-    l->version--;
-    if (bad[0] == 0)
-        return fail(FI_ERR_NONFINITE, "step: the gradient norm is not finite (NaN / Inf in the "
-                                      "batch's losses or gradients); update skipped, parameters unchanged");
+    const int skipped = bad[2], why = bad[3];
+    if (skipped == 0) return FI_OK;
+    FI_HIP_CHECK(hipMemsetAsync(l->bad + 2, 0, 2 * sizeof(int), l->stream));  // ordered before the next step
+    l->step_count -= skipped;
+    l->version -= (uint64_t)skipped;
+    const std::string n = skipped > 1 ? std::to_string(skipped) + " of the enqueued updates skipped" : "update skipped";
+    if (!(why & 1))
+        return fail(FI_ERR_NONFINITE, "step: the gradient norm is not finite (NaN / Inf in the batch's losses or "
+                                      "gradients); " + n + ", parameters unchanged");
+    const std::string acts = bad[0] > 0 ? std::to_string(bad[0]) + " action(s)" : "action(s)";
     if (l->comm && l->nranks > 1)
-        return fail(FI_ERR_INVALID, "step: " + std::to_string(bad[0]) + " action(s) outside [0, " +
-                                        std::to_string(l->A) + ") in the data-parallel group's batch "
-                                        "(all-reduced reject flag); batch rejected on every replica, "
-                                        "parameters unchanged");
-    return fail(FI_ERR_INVALID, "step: " + std::to_string(bad[0]) + " action(s) outside [0, " +
-                                    std::to_string(l->A) + ") in the batch; batch rejected, "
-                                    "parameters unchanged");
+        return fail(FI_ERR_INVALID, "step: " + acts + " outside [0, " + std::to_string(l->A) +
+                                        ") in the data-parallel group's batch (all-reduced reject flag); batch "
+                                        "rejected on every replica, " + n + ", parameters unchanged");
+    return fail(FI_ERR_INVALID, "step: " + acts + " outside [0, " + std::to_string(l->A) + ") in the batch; batch "
+                                "rejected, " + n + ", parameters unchanged");
 }
 
 static void fill_stats(fi_learner* l, fi_step_stats* out) {

@@ -323,13 +323,25 @@ int grad_sqnorm(const float* g, size_t n, double* part, int nblk, double* out, h
 }
 
 // ---------------------------------------------------------------- optimizer
+// skip (the learner's flag words): [0] out-of-range actions in the batch (all-reduced),
+// [1] non-finite gradient norm -- either leaves parameters and moments as they are. A skipped
+// update is also counted in [2] and its reasons OR-ed into [3] (1 = actions, 2 = non-finite)
+// until the host reads them, so a step skipped behind others still in flight (asynchronous
+// submission) is reported by the next wait, not lost.
+__device__ __forceinline__ bool skip_update(int* skip) {
+    if (!skip || (skip[0] | skip[1]) == 0) return false;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        skip[2] += 1;
+        skip[3] |= (skip[0] != 0 ? 1 : 0) | (skip[1] != 0 ? 2 : 0);
+    }
+    return true;
+}
+
 __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                             float* __restrict__ m, float* __restrict__ v, size_t n, float lr,
                             float b1, float b2, float eps, double bc1, double bc2,
-                            const double* sqnorm, float max_norm, const int* skip) {
-    // skip[0]: rejected batch (bad actions), skip[1]: non-finite gradient norm -- parameters
-    // and moments stay as they are
-    if (skip && (skip[0] | skip[1]) != 0) return;
+                            const double* sqnorm, float max_norm, int* skip) {
+    if (skip_update(skip)) return;
     float scale = 1.f;
     if (max_norm > 0.f) {
         const double norm = sqrt(*sqnorm);
@@ -348,8 +360,8 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
 }
 
 __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, size_t n, float lr,
-                           const double* sqnorm, float max_norm, const int* skip) {
-    if (skip && (skip[0] | skip[1]) != 0) return;
+                           const double* sqnorm, float max_norm, int* skip) {
+    if (skip_update(skip)) return;
     float scale = 1.f;
     if (max_norm > 0.f) {
         const double norm = sqrt(*sqnorm);
@@ -362,7 +374,7 @@ __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, s
 
 int optimizer_step(int opt, float* p, const float* g, float* m, float* v, size_t n, float lr,
                    float b1, float b2, float eps, double bc1, double bc2, const double* sqnorm,
-                   float max_norm, hipStream_t s, const int* skip) {
+                   float max_norm, hipStream_t s, int* skip) {
     if (opt == FI_OPT_ADAM)
         hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, s, p, g, m, v, n, lr, b1,
                            b2, eps, bc1, bc2, sqnorm, max_norm, skip);

@@ -109,8 +109,10 @@ int fi_learner_step_resident(fi_learner* l, fi_step_stats* out);
 /* Asynchronous form: copies the entries into one of two pinned
  * buffers, enqueues the H2D copy and the whole step, and returns -- the caller may free the
  * entries and read the next batch while the device works. fi_learner_wait blocks until the
- * last enqueued step is done and reports its statistics (step_ms = 0). Publication calls
- * (fi_learner_get_params*) also see the completed step.                                  */
+ * last enqueued step is done and reports its statistics (step_ms = 0), and fails with
+ * FI_ERR_INVALID / FI_ERR_NONFINITE when any update enqueued since the last check was
+ * skipped (the device counts them; the version counts applied updates only). Publication
+ * calls (fi_learner_get_params*) also see the completed step.                            */
 int fi_learner_step_async(fi_learner* l, const void* const* entries, size_t n_entries,
                           size_t entry_bytes);
 int fi_learner_wait(fi_learner* l, fi_step_stats* out);

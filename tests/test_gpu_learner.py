@@ -472,6 +472,41 @@ def test_nonfinite_gradient_skips_update(orc, monkeypatch, attach, poison):
     R.close()
 
 
+@pytest.mark.parametrize("kind", ["action", "nan"])
+def test_skipped_step_behind_others_in_flight_is_reported(orc, kind):
+    """Three asynchronous steps enqueued back to back (no wait between them), the middle batch
+    bad (an out-of-range action, or a NaN reward). The device counts the skipped update, so the
+    wait after the third step reports it (the flags of the last step alone are clean), the
+    version counts the two applied updates, and the parameters equal a handle that stepped
+    only the two good batches (SGD: no step-number dependence), bit for bit."""
+    from freeimpala_amd._abi import FiError
+    from freeimpala_amd.learner import pack_records
+    T, B = 4, 32
+    good1 = orc.synth_batch(61, T=T, B=B, A=18, D=128)
+    good2 = orc.synth_batch(62, T=T, B=B, A=18, D=128)
+    bad = {k: (None if v is None else v.copy()) for k, v in good1.items()}
+    if kind == "action":
+        bad["actions"][2, 9] = 18
+    else:
+        bad["rewards"][0, 3] = np.nan
+    pk = lambda b: pack_records(b["obs"], b["mu"], b["actions"], b["rewards"], b["discounts"],
+                                entry_size=T + 1)
+    L, R = mk(T=T, B=B, seed=8), mk(T=T, B=B, seed=8)
+    v0 = L.step(pk(good1))["version"]
+    R.step(pk(good1))
+    for b in (good2, bad, good1):
+        L.step_async(pk(b))
+    with pytest.raises(FiError, match="outside" if kind == "action" else "not finite"):
+        L.wait()
+    R.step(pk(good2))
+    r = R.step(pk(good1))
+    np.testing.assert_array_equal(L.get_params(), R.get_params())
+    s = L.step(pk(good2))  # the handle carries on; the skip counter was cleared by the wait
+    assert s["version"] == r["version"] + 1 == v0 + 3
+    L.close()
+    R.close()
+
+
 def _two_devices():
     from freeimpala_amd import hip
     n = hip.device_count()
