@@ -901,7 +901,13 @@ extern "C" int fi_learner_get_params(fi_learner* l, void* dst, size_t bytes, uin
         uint16_t* o = (uint16_t*)dst;
         for (size_t i = 0; i < l->nparams; ++i) o[i] = f2bf(tmp[i]);
     }
-    if (version) *version = l->version;
+    if (version) {
+        // updates skipped by steps not yet checked (asynchronous submission, reported by the
+        // next fi_learner_wait) are not counted, so the published version never goes back
+        int pending = 0;
+        FI_HIP_CHECK(hipMemcpy(&pending, l->bad + 2, sizeof(int), hipMemcpyDeviceToHost));
+        *version = l->version - (uint64_t)pending;
+    }
     return FI_OK;
 }
 
@@ -926,6 +932,7 @@ extern "C" int fi_learner_set_params(fi_learner* l, const void* src, size_t byte
     }
     FI_HIP_CHECK(hipMemcpyAsync(l->params, p, l->nparams * 4, hipMemcpyHostToDevice, l->stream));
     if (l->atari) FI_TRY(atari_sync_weights(l->atari, l->params, l->stream));
+    FI_HIP_CHECK(hipMemsetAsync(l->bad + 2, 0, 2 * sizeof(int), l->stream));  // a new version line
     FI_HIP_CHECK(hipStreamSynchronize(l->stream));
     l->version = version;
     return FI_OK;
@@ -976,6 +983,7 @@ extern "C" int fi_learner_load_state(fi_learner* l, const void* src, size_t byte
     FI_HIP_CHECK(hipMemcpyAsync(l->opt_m, f + l->nparams, l->nparams * 4, hipMemcpyHostToDevice, l->stream));
     FI_HIP_CHECK(hipMemcpyAsync(l->opt_v, f + 2 * l->nparams, l->nparams * 4, hipMemcpyHostToDevice, l->stream));
     if (l->atari) FI_TRY(atari_sync_weights(l->atari, l->params, l->stream));
+    FI_HIP_CHECK(hipMemsetAsync(l->bad + 2, 0, 2 * sizeof(int), l->stream));
     FI_HIP_CHECK(hipStreamSynchronize(l->stream));
     l->step_count = h.step_count;
     l->version = h.version;

@@ -477,7 +477,8 @@ def test_skipped_step_behind_others_in_flight_is_reported(orc, kind):
     """Three asynchronous steps enqueued back to back (no wait between them), the middle batch
     bad (an out-of-range action, or a NaN reward). The device counts the skipped update, so the
     wait after the third step reports it (the flags of the last step alone are clean), the
-    version counts the two applied updates, and the parameters equal a handle that stepped
+    version counts the two applied updates (also when published before the wait: it never goes
+    back), and the parameters equal a handle that stepped
     only the two good batches (SGD: no step-number dependence), bit for bit."""
     from freeimpala_amd._abi import FiError
     from freeimpala_amd.learner import pack_records
@@ -496,8 +497,11 @@ def test_skipped_step_behind_others_in_flight_is_reported(orc, kind):
     R.step(pk(good1))
     for b in (good2, bad, good1):
         L.step_async(pk(b))
+    # publication before the wait sees the completed steps and counts applied updates only
+    assert L.get_blob()[1] == v0 + 2
     with pytest.raises(FiError, match="outside" if kind == "action" else "not finite"):
         L.wait()
+    assert L.get_blob()[1] == v0 + 2
     R.step(pk(good2))
     r = R.step(pk(good1))
     np.testing.assert_array_equal(L.get_params(), R.get_params())
