@@ -216,6 +216,51 @@ def test_atari_action_set_limit():
         mk(A=19)
 
 
+def test_atari_state_resume_is_bit_exact():
+    """Checkpoint / resume of the Atari learner: save_state after two
+    Adam steps, load it into a handle created with another seed, and step both on the same
+    batch. load_state must also rebuild the bf16 weight images the conv / fc / heads kernels
+    read (not only the fp32 master weights), so the resumed step is bit-identical: parameters,
+    both Adam moments, loss and version."""
+    kw = dict(optimizer="adam", lr=5e-4, max_grad_norm=40.0)
+    L1 = mk(T=2, B=8, seed=3, **kw)
+    L1.synth(seed=77)
+    L1.step_resident()
+    L1.step_resident()
+    blob = L1.save_state()
+    L2 = mk(T=2, B=8, seed=99, **kw)
+    L2.synth(seed=77)
+    L2.load_state(blob)
+    a, b = L1.step_resident(), L2.step_resident()
+    np.testing.assert_array_equal(L1.get_params(), L2.get_params())
+    np.testing.assert_array_equal(L1.tensor("adam_m"), L2.tensor("adam_m"))
+    np.testing.assert_array_equal(L1.tensor("adam_v"), L2.tensor("adam_v"))
+    assert a["total_loss"] == b["total_loss"] and a["version"] == b["version"] == 3
+    L1.close()
+    L2.close()
+
+
+@pytest.mark.parametrize("T,B", [(1, 9), (1, 256)])
+def test_atari_single_step_sequences(orc, T, B, monkeypatch):
+    """T = 1 (one transition plus the bootstrap frame per column): the smallest sequence the
+    learner accepts, on the production path, ragged and full-tile batches, against the oracle."""
+    for k in ("FI_KEEP_DA1", "FI_A1_NHWC", "FI_FWD_UNFUSED", "FI_BWD_UNFUSED", "FI_FR_GRID"):
+        monkeypatch.delenv(k, raising=False)
+    N = (T + 1) * B
+    monkeypatch.setenv("FI_KEEP_DA1", "1")
+    twin = mk(T=T, B=B, seed=29)
+    monkeypatch.delenv("FI_KEEP_DA1")
+    L = mk(T=T, B=B, seed=29)
+    for x in (twin, L):
+        x.synth(seed=1000 + B)
+    twin.step_resident()
+    da1 = bf16_to_f32(twin.tensor("da1", np.uint16, (N, 20, 20, 32)))
+    g = _check_step_against_oracle(orc, L, T, B, 18, a1_planar=True, da1=da1)
+    np.testing.assert_array_equal(g, twin.tensor("grads"))
+    twin.close()
+    L.close()
+
+
 def test_atari_training_reduces_loss():
     """gamma = 0 makes the V-trace target the (clipped) immediate reward, so the value loss of a
     fixed batch is a plain regression that SGD must reduce."""
