@@ -261,6 +261,39 @@ def test_atari_single_step_sequences(orc, T, B, monkeypatch):
     L.close()
 
 
+def test_two_atari_players_step_concurrently():
+    """Two players (the reference runs one worker thread per player, learner.h:158-163) with
+    Atari handles on one GPU, stepping from two host threads at once (the ABI releases the GIL;
+    each handle has its own stream, slabs and staging): every result is bit-identical to the
+    same handles stepped one after the other."""
+    import threading
+    def run(concurrent):
+        Ls = [mk(T=2, B=24, seed=41 + p, optimizer="adam") for p in range(2)]
+        for p, L in enumerate(Ls):
+            L.synth(seed=500 + p)
+        out = [None, None]
+        def work(p):
+            for _ in range(3):
+                out[p] = Ls[p].step_resident()
+        if concurrent:
+            th = [threading.Thread(target=work, args=(p,)) for p in range(2)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+        else:
+            work(0)
+            work(1)
+        res = [(L.get_params(), o["total_loss"]) for L, o in zip(Ls, out)]
+        for L in Ls:
+            L.close()
+        return res
+    seq, par = run(False), run(True)
+    for (pa, la), (pb, lb) in zip(seq, par):
+        np.testing.assert_array_equal(pa, pb)
+        assert la == lb
+
+
 def test_atari_training_reduces_loss():
     """gamma = 0 makes the V-trace target the (clipped) immediate reward, so the value loss of a
     fixed batch is a plain regression that SGD must reduce."""
