@@ -1,21 +1,30 @@
 // metrics.hpp -- the learner's counters of freeimpala's MetricsTracker, natively.
 //
 // Reference include/freeimpala/metrics_tracker.h: a process-wide singleton; counters only count
-// between start() and stop(); createTrainingTimer() returns a scoped timer whose destructor
-// adds the elapsed ns to the training time (:131-134, :146-169); recordLearnerModelUpdate()
-// counts published models (:109-112). The learner step also reports what the device did:
-// env-steps trained (T x B per step) and device milliseconds, so the summary can state
-// env-steps/s next to the reference's counters.
+// between start() and stop(); scoped timers add their elapsed ns to the simulation / training /
+// transfer / sync times (:126-177); recordLearnerModelUpdate() counts published models
+// (:109-112); per-agent iteration times (:92-107); rates and the time distribution (:205-254);
+// saveMetricsToCSV writes the reference's "Metric,Value" file (:265-329), which cmd/freeimpala
+// writes for --metrics-file (main.cpp:254-257). The learner step also reports what the device
+// did: env-steps trained (T x B per step), device milliseconds and rejected batches, appended
+// as rows of their own so the file states env-steps/s next to the reference's counters.
+// Unlike the reference, an agent iteration's start time is per thread (the reference keeps one
+// start time for every agent thread), and the execution time stops at stop().
 #pragma once
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
+#include <fstream>
 #include <functional>
+#include <limits>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <vector>
 
 namespace freeimpala_amd {
 
@@ -54,8 +63,42 @@ public:
     ScopedTimer createTrainingTimer() {
         return ScopedTimer([this](uint64_t ns) { recordTrainingTime(ns); });
     }
+    ScopedTimer createSimulationTimer() {
+        return ScopedTimer([this](uint64_t ns) { recordSimulationTime(ns); });
+    }
+    ScopedTimer createTransferTimer() {
+        return ScopedTimer([this](uint64_t ns) { recordTransferTime(ns); });
+    }
+    ScopedTimer createSyncTimer() {
+        return ScopedTimer([this](uint64_t ns) { recordSyncTime(ns); });
+    }
     void recordTrainingTime(uint64_t ns) {
         if (running_.load()) training_ns_ += ns;
+    }
+    void recordSimulationTime(uint64_t ns) {
+        if (running_.load()) simulation_ns_ += ns;
+    }
+    void recordTransferTime(uint64_t ns) {
+        if (running_.load()) transfer_ns_ += ns;
+    }
+    void recordSyncTime(uint64_t ns) {
+        if (running_.load()) sync_ns_ += ns;
+    }
+    // one agent iteration (agent.h:236, :290): the start time is the calling thread's own
+    void startAgentIteration(size_t) {
+        if (running_.load()) iter_start() = Clock::now();
+    }
+    void endAgentIteration(size_t agent_id) {
+        if (!running_.load()) return;
+        const uint64_t ns =
+            (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - iter_start()).count();
+        std::lock_guard<std::mutex> lk(mu_);
+        AgentTimes& a = agents_[agent_id];
+        a.total += ns;
+        a.count++;
+        a.min = std::min(a.min, ns);
+        a.max = std::max(a.max, ns);
+        iterations_++;
     }
     void recordLearnerModelUpdate() {
         if (running_.load()) model_updates_++;
@@ -91,6 +134,63 @@ public:
         const auto end = running_.load() ? Clock::now() : t1_;
         return std::chrono::duration<double>(end - t0_).count();
     }
+    uint64_t getTotalExecutionTime() const { return (uint64_t)(getElapsedSeconds() * 1e9); }
+    uint64_t getTotalIterations() const { return iterations_.load(); }
+    uint64_t getTotalSimulationTime() const { return simulation_ns_.load(); }
+    uint64_t getTotalTransferTime() const { return transfer_ns_.load(); }
+    uint64_t getTotalSyncTime() const { return sync_ns_.load(); }
+    double getIterationsPerSecond() const { return per_second(getTotalIterations()); }
+    double getLearnerUpdatesPerSecond() const { return per_second(getTotalLearnerModelUpdates()); }
+    double getAgentSyncsPerSecond() const { return per_second(getTotalAgentModelSyncs()); }
+    double getDataTransfersPerSecond() const { return per_second(getTotalDataTransfers()); }
+    double getLearnerEnvStepsPerSecond() const { return per_second(getTotalLearnerEnvSteps()); }
+    // shares of the four timed activities, in percent (metrics_tracker.h:235-254)
+    std::map<std::string, double> getTimeDistribution() const {
+        const double sim = (double)getTotalSimulationTime(), tr = (double)getTotalTrainingTime(),
+                     xf = (double)getTotalTransferTime(), sy = (double)getTotalSyncTime();
+        const double tot = sim + tr + xf + sy;
+        auto pct = [tot](double v) { return tot > 0 ? 100.0 * v / tot : 0.0; };
+        return {{"simulation", pct(sim)}, {"training", pct(tr)}, {"transfer", pct(xf)}, {"sync", pct(sy)}};
+    }
+
+    // the reference's --metrics-file (metrics_tracker.h:265-329), then the device learner's rows
+    bool saveMetricsToCSV(const std::string& filename) const {
+        std::ofstream f(filename);
+        if (!f) {
+            std::fprintf(stderr, "Could not open file for writing: %s\n", filename.c_str());
+            return false;
+        }
+        f << "Metric,Value\n";
+        f << "TotalExecutionTime_ns," << getTotalExecutionTime() << "\n";
+        f << "TotalSimulationTime_ns," << getTotalSimulationTime() << "\n";
+        f << "TotalTrainingTime_ns," << getTotalTrainingTime() << "\n";
+        f << "TotalTransferTime_ns," << getTotalTransferTime() << "\n";
+        f << "TotalSyncTime_ns," << getTotalSyncTime() << "\n";
+        f << "TotalIterations," << getTotalIterations() << "\n";
+        f << "TotalLearnerModelUpdates," << getTotalLearnerModelUpdates() << "\n";
+        f << "TotalAgentModelSyncs," << getTotalAgentModelSyncs() << "\n";
+        f << "TotalDataTransfers," << getTotalDataTransfers() << "\n";
+        f << "IterationsPerSecond," << getIterationsPerSecond() << "\n";
+        f << "LearnerUpdatesPerSecond," << getLearnerUpdatesPerSecond() << "\n";
+        f << "AgentSyncsPerSecond," << getAgentSyncsPerSecond() << "\n";
+        f << "DataTransfersPerSecond," << getDataTransfersPerSecond() << "\n";
+        for (const auto& [key, value] : getTimeDistribution()) f << "TimePercentage_" << key << "," << value << "\n";
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            for (const auto& [id, a] : agents_) {
+                if (a.count == 0) continue;
+                f << "Agent_" << id << "_TotalTime_ns," << a.total << "\n";
+                f << "Agent_" << id << "_AvgIterationTime_ns," << (double)a.total / (double)a.count << "\n";
+                f << "Agent_" << id << "_MinIterationTime_ns," << a.min << "\n";
+                f << "Agent_" << id << "_MaxIterationTime_ns," << a.max << "\n";
+            }
+        }
+        f << "TotalLearnerEnvSteps," << getTotalLearnerEnvSteps() << "\n";
+        f << "LearnerEnvStepsPerSecond," << getLearnerEnvStepsPerSecond() << "\n";
+        f << "TotalDeviceTime_ms," << getTotalDeviceMs() << "\n";
+        f << "TotalRejectedBatches," << getTotalRejectedBatches() << "\n";
+        return (bool)f;
+    }
 
     // one JSON object with every counter (the CLI prints it as its summary line)
     std::string summaryJson() const {
@@ -112,12 +212,24 @@ public:
 
 private:
     MetricsTracker() = default;
+    struct AgentTimes {
+        uint64_t total = 0, count = 0, min = std::numeric_limits<uint64_t>::max(), max = 0;
+    };
+    static Clock::time_point& iter_start() {
+        thread_local Clock::time_point t{};
+        return t;
+    }
+    double per_second(uint64_t n) const {
+        const double s = getElapsedSeconds();
+        return s > 0 ? (double)n / s : 0.0;
+    }
     std::atomic<bool> running_{false};
     Clock::time_point t0_{}, t1_{};
-    std::atomic<uint64_t> training_ns_{0}, model_updates_{0}, data_transfers_{0}, agent_syncs_{0},
-        env_steps_{0}, rejected_{0};
+    std::atomic<uint64_t> training_ns_{0}, simulation_ns_{0}, transfer_ns_{0}, sync_ns_{0}, model_updates_{0},
+        data_transfers_{0}, agent_syncs_{0}, env_steps_{0}, rejected_{0}, iterations_{0};
     mutable std::mutex mu_;
     double device_ms_ = 0.0;
+    std::map<size_t, AgentTimes> agents_;
 };
 
 }  // namespace freeimpala_amd

@@ -9,7 +9,8 @@
 //   * Model / ModelManager (:43-157, :310-481): one publisher against readers copying the model
 //     (no torn copy: every blob byte equals its version's pattern), version polling, waits, and
 //     concurrent checkpoint saves of one player;
-//   * MetricsTracker (metrics_tracker.h): scoped timers and counters from many threads;
+//   * MetricsTracker (metrics_tracker.h): scoped timers, counters and agent iterations from many
+//     threads while the --metrics-file CSV is written;
 //   * SimLearner (learner.h:32-197, config #1's learner): worker threads, checkpoint threads,
 //     actor threads writing entries and syncing the published model, stop().
 // No GPU: nothing here calls the C ABI. Prints "OK race" and exits 0 when every check holds.
@@ -170,24 +171,38 @@ static int model_stress(const std::string& dir) {
     return 0;
 }
 
-static int metrics_stress() {
+static int metrics_stress(const std::string& dir) {
     auto m = MetricsTracker::getInstance();
     m->start();
     const uint64_t u0 = m->getTotalLearnerModelUpdates(), t0 = m->getTotalDataTransfers();
     std::vector<std::thread> ts;
+    const uint64_t i0 = m->getTotalIterations();
     for (int i = 0; i < 8; ++i)
-        ts.emplace_back([&] {
+        ts.emplace_back([&, i] {
             for (int k = 0; k < 500; ++k) {
-                auto timer = m->createTrainingTimer();
-                m->recordLearnerModelUpdate();
-                m->recordDataTransfer();
-                m->recordAgentModelSync();
-                m->recordLearnerEnvSteps(100, 0.01);
+                m->startAgentIteration((size_t)i);  // per-thread start time (agent.h:236, :290)
+                {
+                    auto timer = m->createTrainingTimer();
+                    m->recordLearnerModelUpdate();
+                    m->recordDataTransfer();
+                    m->recordAgentModelSync();
+                    m->recordLearnerEnvSteps(100, 0.01);
+                }
+                { auto s = m->createSimulationTimer(); }
+                { auto x = m->createTransferTimer(); }
+                { auto y = m->createSyncTimer(); }
+                m->endAgentIteration((size_t)i);
             }
         });
+    // the --metrics-file writer reading every counter while they move
+    std::thread writer([&] {
+        for (int k = 0; k < 20; ++k) m->saveMetricsToCSV(dir + "/metrics.csv");
+    });
     for (auto& t : ts) t.join();
+    writer.join();
     m->stop();
     CHECK(m->getTotalLearnerModelUpdates() - u0 == 4000 && m->getTotalDataTransfers() - t0 == 4000);
+    CHECK(m->getTotalIterations() - i0 == 4000);
     return 0;
 }
 
@@ -231,7 +246,7 @@ static int sim_learner_stress(const std::string& dir) {
 
 int main(int argc, char** argv) {
     const std::string dir = argc > 1 ? argv[1] : "/tmp/fi_race_check";
-    if (buffer_stress() || model_stress(dir + "/models") || metrics_stress() || sim_learner_stress(dir + "/sim")) return 1;
+    if (buffer_stress() || model_stress(dir + "/models") || (std::filesystem::create_directories(dir), metrics_stress(dir)) || sim_learner_stress(dir + "/sim")) return 1;
     std::printf("OK race\n");
     return 0;
 }

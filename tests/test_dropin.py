@@ -83,9 +83,28 @@ def test_config1_reference_learner_sim_on_cpu(tmp_path):
     and --game-steps 100, as in the survey's measurement (4 learner
     updates, ~1.7 k env-steps/s, sleep-bound)."""
     ck = tmp_path / "ck"
+    csv = tmp_path / "metrics.csv"
     r = run(["--players", "1", "--iterations", "32", "--buffer-capacity", "32", "--batch-size", "32",
-             "--agents", "4", "--learner", "sim", "--checkpoint-location", str(ck)], timeout=120)
+             "--agents", "4", "--learner", "sim", "--checkpoint-location", str(ck),
+             "--metrics-file", str(csv)], timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
+    # --metrics-file: the reference's "Metric,Value" CSV (metrics_tracker.h:265-329) with the
+    # device learner's rows appended; the counters of the reference's typical checks
+    # (SURVEY.md section 4): transfers = agents x iterations x players, updates = floor(A*T/M)
+    lines = csv.read_text().splitlines()
+    assert lines[0] == "Metric,Value"
+    m = dict(ln.split(",", 1) for ln in lines[1:])
+    for k in ("TotalExecutionTime_ns", "TotalSimulationTime_ns", "TotalTrainingTime_ns", "TotalTransferTime_ns",
+              "TotalSyncTime_ns", "IterationsPerSecond", "LearnerUpdatesPerSecond", "AgentSyncsPerSecond",
+              "DataTransfersPerSecond", "TimePercentage_simulation", "TimePercentage_training",
+              "TimePercentage_transfer", "TimePercentage_sync", "Agent_0_AvgIterationTime_ns",
+              "Agent_3_MaxIterationTime_ns", "TotalLearnerEnvSteps", "LearnerEnvStepsPerSecond"):
+        assert k in m, k
+    assert int(m["TotalIterations"]) == 4 * 32 and int(m["TotalDataTransfers"]) == 4 * 32
+    assert int(m["TotalLearnerModelUpdates"]) == 4
+    # 4 x 32 agent iterations of >= 200 ms simulated play, 4 learner steps of >= 500 ms
+    assert int(m["TotalSimulationTime_ns"]) >= 4 * 32 * 200e6 and int(m["TotalTrainingTime_ns"]) >= 4 * 500e6
+    assert abs(sum(float(m["TimePercentage_" + k]) for k in ("simulation", "training", "transfer", "sync")) - 100) < 1e-3
     out = json.loads(r.stdout.strip().splitlines()[-1])
     assert out["learner"] == "sim" and out["learner_iterations"] == [4] and out["expected_iterations"] == 4
     assert out["param_bytes"] == 1024 * 1024

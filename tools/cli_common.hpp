@@ -120,7 +120,7 @@ inline void setup_parser(ArgumentParser& program, const std::string& description
     program.add_argument("-a", "--agents").help("Number of agent processes").default_value(4).scan<'i', int>();
     program.add_argument("--game-steps").help("Number of steps in each game simulation").default_value(100).scan<'i', int>();
     program.add_argument("--agent-time").help("Simulated game play time for agents (in ms)").default_value(200).scan<'i', int>();
-    program.add_argument("--metrics-file").help("File to save performance metrics (JSON)").default_value(std::string(""));
+    program.add_argument("--metrics-file").help("File to save performance metrics (CSV)").default_value(std::string(""));
     program.add_argument("--seed").help("Seed for random number generation")
         .default_value(static_cast<unsigned>(std::time(nullptr))).scan<'u', unsigned>();
     program.add_argument("--log-level").help("Set the logging level").default_value(std::string("info"))
@@ -240,13 +240,11 @@ private:
     std::vector<std::vector<char>> entries_;
 };
 
-// the run's closing JSON line (stdout and --metrics-file)
+// the run's closing JSON line on stdout; --metrics-file gets the reference's CSV
+// (MetricsTracker::saveMetricsToCSV, cmd/freeimpala/main.cpp:254-257)
 inline void report(const Params& P, const std::string& line) {
     std::cout << line << std::endl;
-    if (!P.metrics_file.empty()) {
-        std::ofstream f(P.metrics_file);
-        f << line << "\n";
-    }
+    if (!P.metrics_file.empty()) MetricsTracker::getInstance()->saveMetricsToCSV(P.metrics_file);
 }
 
 template <class L>

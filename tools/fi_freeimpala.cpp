@@ -43,21 +43,35 @@ public:
         for (size_t p = 0; p < P.num_players; ++p) versions_[p] = models_->getLatestVersion(p);
     }
 
+    // the reference agent's loop and its metric hooks (agent.h:34-98, 154-181, 236-290): a timed
+    // simulation, a timed transfer per player, a timed model sync, one timed iteration
     void run() {
         auto metrics = MetricsTracker::getInstance();
         for (size_t it = 0; it < P_.total_iterations; ++it) {
-            if (P_.agent_time) std::this_thread::sleep_for(std::chrono::milliseconds(P_.agent_time));
-            auto& entries = game_.play(versions_);
+            metrics->startAgentIteration(id_);
+            std::vector<std::vector<char>>* entries = nullptr;
+            {
+                auto timer = metrics->createSimulationTimer();
+                if (P_.agent_time) std::this_thread::sleep_for(std::chrono::milliseconds(P_.agent_time));
+                entries = &game_.play(versions_);
+            }
             for (size_t p = 0; p < P_.num_players; ++p) {
-                if (bufs_[p]->write(entries[p])) metrics->recordDataTransfer();
+                auto timer = metrics->createTransferTimer();
+                if (bufs_[p]->write((*entries)[p])) metrics->recordDataTransfer();
                 else std::fprintf(stderr, "[agent %zu] failed to write data for player %zu\n", id_, p);
-                const uint64_t latest = models_->getLatestVersion(p);
-                if (latest > versions_[p]) {
-                    local_ = models_->getModel(p)->getData();  // the actor's copy of the policy
-                    versions_[p] = latest;
-                    metrics->recordAgentModelSync();
+            }
+            {
+                auto timer = metrics->createSyncTimer();
+                for (size_t p = 0; p < P_.num_players; ++p) {
+                    const uint64_t latest = models_->getLatestVersion(p);
+                    if (latest > versions_[p]) {
+                        local_ = models_->getModel(p)->getData();  // the actor's copy of the policy
+                        versions_[p] = latest;
+                        metrics->recordAgentModelSync();
+                    }
                 }
             }
+            metrics->endAgentIteration(id_);
         }
     }
 
