@@ -15,6 +15,7 @@
 //     actor threads writing entries and syncing the published model, stop().
 // No GPU: nothing here calls the C ABI. Prints "OK race" and exits 0 when every check holds.
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <filesystem>
@@ -61,9 +62,9 @@ static int buffer_stress() {
             for (int s = 0; s < PER; ++s) {
                 const auto e = tagged(1024, (uint32_t)w, (uint32_t)s);
                 bool ok = (w & 1) ? sb.write(e) : false;
-                while (!ok) {  // even writers spin on try_write (mpi_async_pool-style producers)
-                    ok = sb.try_write(e);
-                    if (!ok) std::this_thread::yield();
+                while (!ok) {  // even writers retry try_write (mpi_async_pool-style producers); a
+                    ok = sb.try_write(e);  // short sleep, not a yield: under TSAN a yield spin can
+                    if (!ok) std::this_thread::sleep_for(std::chrono::microseconds(20));  // starve the lock holder
                 }
                 written.fetch_add(1);
             }
