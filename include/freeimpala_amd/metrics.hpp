@@ -8,8 +8,9 @@
 // writes for --metrics-file (main.cpp:254-257). The learner step also reports what the device
 // did: env-steps trained (T x B per step), device milliseconds and rejected batches, appended
 // as rows of their own so the file states env-steps/s next to the reference's counters.
-// Unlike the reference, an agent iteration's start time is per thread (the reference keeps one
-// start time for every agent thread), and the execution time stops at stop().
+// printMetricsSummary is the reference's end-of-run report (:332-382) with a learner section.
+// An agent iteration's start time is per thread, as in the reference (:388); unlike the
+// reference, the execution time stops at stop().
 #pragma once
 
 #include <algorithm>
@@ -84,7 +85,7 @@ public:
     void recordSyncTime(uint64_t ns) {
         if (running_.load()) sync_ns_ += ns;
     }
-    // one agent iteration (agent.h:236, :290): the start time is the calling thread's own
+    // one agent iteration (agent.h:236, :290): the start time is the calling thread's own (:388)
     void startAgentIteration(size_t) {
         if (running_.load()) iter_start() = Clock::now();
     }
@@ -190,6 +191,50 @@ public:
         f << "TotalDeviceTime_ms," << getTotalDeviceMs() << "\n";
         f << "TotalRejectedBatches," << getTotalRejectedBatches() << "\n";
         return (bool)f;
+    }
+
+    // the reference's end-of-run report (metrics_tracker.h:332-382), then the device learner's
+    void printMetricsSummary() const {
+        std::string o = "\n===== Performance Metrics Summary =====\n";
+        char b[160];
+        auto line = [&](const char* fmt, double v) {
+            std::snprintf(b, sizeof b, fmt, v);
+            o += b;
+        };
+        line("Total Execution Time: %.3f seconds\n", getTotalExecutionTime() / 1e9);
+        o += "\n--- Throughput Metrics ---\n";
+        line("Iterations Per Second: %.2f\n", getIterationsPerSecond());
+        line("Learner Model Updates Per Second: %.2f\n", getLearnerUpdatesPerSecond());
+        line("Agent Model Syncs Per Second: %.2f\n", getAgentSyncsPerSecond());
+        line("Data Transfers Per Second: %.2f\n", getDataTransfersPerSecond());
+        o += "\n--- Time Distribution ---\n";
+        for (const auto& [key, value] : getTimeDistribution()) {
+            std::snprintf(b, sizeof b, "%s: %.1f%%\n", key.c_str(), value);
+            o += b;
+        }
+        o += "\n--- Total Counts ---\n";
+        o += "Total Iterations: " + std::to_string(getTotalIterations()) + "\n";
+        o += "Total Learner Model Updates: " + std::to_string(getTotalLearnerModelUpdates()) + "\n";
+        o += "Total Agent Model Syncs: " + std::to_string(getTotalAgentModelSyncs()) + "\n";
+        o += "Total Data Transfers: " + std::to_string(getTotalDataTransfers()) + "\n";
+        o += "\n--- Per-Agent Metrics ---\n";
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            for (const auto& [id, a] : agents_) {
+                if (a.count == 0) continue;
+                std::snprintf(b, sizeof b, "Agent %zu Avg Iteration Time: %.3f ms\n", id,
+                              (double)a.total / (double)a.count / 1e6);
+                o += b;
+            }
+        }
+        o += "\n--- Device Learner ---\n";
+        o += "Total Learner Env-Steps: " + std::to_string(getTotalLearnerEnvSteps()) + "\n";
+        line("Learner Env-Steps Per Second: %.1f\n", getLearnerEnvStepsPerSecond());
+        line("Device Time: %.3f ms\n", getTotalDeviceMs());
+        o += "Rejected Batches: " + std::to_string(getTotalRejectedBatches()) + "\n";
+        o += "=====================================\n";
+        std::fputs(o.c_str(), stdout);
+        std::fflush(stdout);
     }
 
     // one JSON object with every counter (the CLI prints it as its summary line)

@@ -91,6 +91,7 @@ def test_config1_reference_learner_sim_on_cpu(tmp_path):
     # --metrics-file: the reference's "Metric,Value" CSV (metrics_tracker.h:265-329) with the
     # device learner's rows appended; the counters of the reference's typical checks
     # (SURVEY.md section 4): transfers = agents x iterations x players, updates = floor(A*T/M)
+    assert "===== Performance Metrics Summary =====" in r.stdout  # metrics_tracker.h:332-382
     lines = csv.read_text().splitlines()
     assert lines[0] == "Metric,Value"
     m = dict(ln.split(",", 1) for ln in lines[1:])

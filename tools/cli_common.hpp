@@ -240,9 +240,11 @@ private:
     std::vector<std::vector<char>> entries_;
 };
 
-// the run's closing JSON line on stdout; --metrics-file gets the reference's CSV
+// the reference's metrics summary, then the run's closing JSON line on stdout (the last line);
+// --metrics-file gets the reference's CSV
 // (MetricsTracker::saveMetricsToCSV, cmd/freeimpala/main.cpp:254-257)
 inline void report(const Params& P, const std::string& line) {
+    MetricsTracker::getInstance()->printMetricsSummary();  // main.cpp:252
     std::cout << line << std::endl;
     if (!P.metrics_file.empty()) MetricsTracker::getInstance()->saveMetricsToCSV(P.metrics_file);
 }
